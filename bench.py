@@ -1,0 +1,198 @@
+"""Benchmark: rows scanned/s + achieved HBM GB/s of a filter + group-by query (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], 1B rows in 100 segments per GPU): each rank holds
+--segments immutable segments of --rows rows of the AdAnalytics-style table in HBM
+(pinot_amd/datagen.py: two fixed-bit dictionary-encoded columns, raw INT/LONG/DOUBLE metrics) and
+runs the filter + group-by query pinot_amd.datagen.BENCH_QUERY over all of them. A step is one full
+execution of that query over the rank's segments (one batched scan kernel over 1B rows) plus, for
+N > 1, the RCCL all-reduce of the dense group tables. Segments are independent, so per-GPU work is
+fixed as N grows (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seg_rows: int, seconds: float):
+    """Time the CPU oracle (scalar C port of the reference path, 1 core) on freshly generated
+    segments of the same workload until `seconds` of CPU work have run."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from pinot_amd import datagen
+    rows = 0
+    t_cpu = 0.0
+    k = 0
+    while t_cpu < seconds and k < 8:
+        bufs = datagen.ad_segment(f"cpu{k}", seg_rows, seed=10_000 + k)
+        t0 = time.perf_counter()
+        oracle.execute(datagen.BENCH_QUERY, [bufs])
+        t_cpu += time.perf_counter() - t0
+        rows += seg_rows
+        k += 1
+    return {"value": rows / t_cpu, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{k} segments x {seg_rows} rows of the same table and query, oracle/pinot_oracle.c "
+                      f"(scalar restatement of the reference Java path), {t_cpu:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--segments", type=int, default=100)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="rows per segment")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify one segment against the oracle")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from pinot_amd import datagen, dist as pdist, engine
+
+    rank, world, local = pdist.init_distributed()
+    torch.cuda.set_device(local)
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+
+    # ---- stage this rank's segments into HBM ----
+    t0 = time.time()
+    segs = []
+    for i in range(args.segments):
+        bufs = datagen.ad_segment(f"adAnalytics_{rank}_{i}", args.rows, seed=rank * 100_003 + i)
+        segs.append(engine.ImmutableSegment(bufs))
+        del bufs
+        if i % 20 == 19:
+            log(f"[rank {rank}] staged {i + 1}/{args.segments} segments ({time.time() - t0:.0f}s)")
+    hbm = sum(s.device_bytes() for s in segs)
+    log(f"[rank {rank}] {args.segments} segments, {hbm / 1e9:.1f} GB in HBM, staged in {time.time() - t0:.0f}s")
+
+    stream = torch.cuda.current_stream()
+    ex = engine.ServerQueryExecutor()
+    res = ex.execute(datagen.BENCH_QUERY, segs, stream=stream)
+    scratch = None
+
+    def step():
+        nonlocal scratch
+        res.execute_again(stream)
+        if world > 1:
+            scratch = pdist.merge_result(res, scratch, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(res.last_kernel_ms())  # HIP events around the scan kernel on `stream`
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    rows_per_rank = args.segments * args.rows
+    total_rows = rows_per_rank * world * args.steps
+    value = total_rows / elapsed
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    alg_bytes = rows_per_rank * datagen.BENCH_BYTES_PER_ROW   # per launch (one launch = all segments)
+    achieved = alg_bytes / avg_kernel_s / 1e9
+
+    groups = res.groups()
+    matched = res.num_docs_matched()
+    if world > 1:
+        m = torch.tensor([matched], dtype=torch.int64, device="cuda")
+        dist.all_reduce(m)
+        matched_all = int(m.item())
+    else:
+        matched_all = matched
+    # size-independent property: the merged group COUNTs add up to the docs that passed the filter
+    assert sum(p[0] for p in groups.values()) == matched_all, "sum of group COUNTs != matched docs"
+
+    if args.check and rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        one = datagen.ad_segment("check", min(args.rows, 2_000_000), seed=424242)
+        r1 = ex.execute(datagen.BENCH_QUERY, [engine.ImmutableSegment(one)]).groups()
+        _, o1 = oracle.execute(datagen.BENCH_QUERY, [one])
+        assert set(r1) == set(o1) and all(r1[k][:3] == o1[k][:3] and r1[k][4] == o1[k][4] for k in o1)
+        log("[check] HIP result == oracle on a 2M-row segment")
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            log("[rank 0] timing the CPU baseline ...")
+            cpu = cpu_baseline(min(args.rows, 10_000_000), args.cpu_seconds)
+        out = {
+            "metric": "rows scanned/sec + achieved HBM GB/s, filter+group-by query, 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/int64/f64",
+            "data": "synthetic (device-generated segments in Pinot's on-disk formats)",
+            "config": {
+                "workload": "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE "
+                            "columns; filter+group-by query",
+                "query": datagen.BENCH_QUERY,
+                "segments_per_gpu": args.segments,
+                "rows_per_segment": args.rows,
+                "rows_per_gpu": rows_per_rank,
+                "selectivity": matched / rows_per_rank,
+                "groups": len(groups),
+                "parallelism": f"segments sharded over {world} GPU(s), RCCL all-reduce merge" if world > 1
+                               else "1 GPU",
+                "hbm_bytes_per_gpu": hbm,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "pamd::scan_kernel<true,false>",
+                "kernel_ms": avg_kernel_s * 1e3,
+                "bytes_per_row": datagen.BENCH_BYTES_PER_ROW,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

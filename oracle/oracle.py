@@ -1,0 +1,337 @@
+"""ctypes driver of the CPU oracle (libpinot_oracle.so). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module; the
+product path (pinot_amd/) never imports it.
+
+The predicate resolution below is an independent Python restatement of
+pinot-core/.../operator/filter/predicate/PredicateEvaluatorProvider.java and the factories it
+calls (RangePredicateEvaluatorFactory, InPredicateEvaluatorFactory, EqualsPredicateEvaluatorFactory,
+NotEquals/NotIn): dictionary-encoded columns resolve values to dictIds, raw columns keep values
+with RANGE bounds normalised to inclusive ones. The per-doc work happens in pinot_oracle.c.
+"""
+from __future__ import annotations
+
+import bisect
+import ctypes as C
+import math
+import os
+import subprocess
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from pinot_amd.query import QueryContext, merge_partial, parse_sql, reduce_rows
+from pinot_amd.segment import (DOUBLE, FLOAT, INT, LONG, STRING, ColumnBuffers, SegmentBuffers,
+                               parse_raw_fwd_header)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libpinot_oracle.so")
+
+OR_TYPE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3}
+OR_ENC = {"FIXED_BIT": 0, "RAW": 1, "SORTED": 2}
+DICT_RANGE, DICT_SET, RAW_RANGE, RAW_IN, DOC_BITSET = 0, 1, 2, 3, 4
+AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4}
+
+
+class OColumn(C.Structure):
+    _fields_ = [("encoding", C.c_int32), ("stored_type", C.c_int32), ("bits", C.c_int32), ("cardinality", C.c_int32),
+                ("fwd", C.c_void_p), ("dict", C.c_void_p)]
+
+
+class OLeaf(C.Structure):
+    _fields_ = [("column", C.c_int32), ("kind", C.c_int32), ("negate", C.c_int32), ("clause", C.c_int32),
+                ("lo_i", C.c_int64), ("hi_i", C.c_int64), ("lo_d", C.c_double), ("hi_d", C.c_double),
+                ("dict_mask", C.c_void_p), ("set_i", C.c_void_p), ("set_d", C.c_void_p), ("set_n", C.c_int32),
+                ("doc_bitset", C.c_void_p)]
+
+
+class OAgg(C.Structure):
+    _fields_ = [("func", C.c_int32), ("column", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-C", HERE, "-s"], check=True)
+        L = C.CDLL(LIB)
+        P, I64 = C.c_void_p, C.c_int64
+        L.oracle_fixedbit_read.restype = C.c_int32
+        L.oracle_fixedbit_read.argtypes = [P, C.c_int32, I64]
+        L.oracle_fixedbit_read_range.argtypes = [P, C.c_int32, I64, I64, P]
+        L.oracle_fixedbit_write.argtypes = [P, C.c_int32, I64, I64, P]
+        L.oracle_sorted_dict_id.restype = C.c_int32
+        L.oracle_sorted_dict_id.argtypes = [P, C.c_int32, I64]
+        L.oracle_raw_read_i64.restype = I64
+        L.oracle_raw_read_i64.argtypes = [P, C.c_int32, I64]
+        L.oracle_raw_read_f64.restype = C.c_double
+        L.oracle_raw_read_f64.argtypes = [P, C.c_int32, I64]
+        L.oracle_column_dict_ids.argtypes = [C.POINTER(OColumn), I64, I64, P]
+        L.oracle_roaring_to_bitset.argtypes = [P, I64, P, I64]
+        L.oracle_inverted_to_bitset.argtypes = [P, C.c_int32, P, C.c_int32, P, I64]
+        L.oracle_filter.restype = I64
+        L.oracle_filter.argtypes = [C.POINTER(OColumn), I64, C.POINTER(OLeaf), C.c_int32, P]
+        L.oracle_bitset_to_doc_ids.restype = I64
+        L.oracle_bitset_to_doc_ids.argtypes = [P, I64, P]
+        L.oracle_aggregate.argtypes = [C.POINTER(OColumn), I64, P, C.POINTER(OAgg), C.c_int32, P, P]
+        L.oracle_group_by.restype = I64
+        L.oracle_group_by.argtypes = [C.POINTER(OColumn), I64, P, P, C.c_int32, C.POINTER(OAgg), C.c_int32, I64, P,
+                                      P, P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# -------------------------------------------------------------------------------- predicate resolution
+def _java_key(s: str) -> bytes:
+    return s.encode("utf-16-be")
+
+
+def _coerce(v, t):
+    if t == STRING:
+        return str(v)
+    if t in (INT, LONG):
+        return int(v)
+    return float(v)
+
+
+def _dict_positions(col: ColumnBuffers, values) -> List[int]:
+    """Dictionary.indexOf for each value; values absent from the dictionary are dropped."""
+    d = col.dict_values
+    out = []
+    if col.stored_type == STRING:
+        keys = [_java_key(x) for x in d]
+        for v in values:
+            k = _java_key(_coerce(v, STRING))
+            i = bisect.bisect_left(keys, k)
+            if i < len(keys) and keys[i] == k:
+                out.append(i)
+    else:
+        for v in values:
+            x = _coerce(v, col.stored_type)
+            i = int(np.searchsorted(d, x, side="left"))
+            if i < len(d) and d[i] == x:
+                out.append(i)
+    return sorted(set(out))
+
+
+def _dict_range(col: ColumnBuffers, p):
+    """SortedDictionaryBasedRangePredicateEvaluator: [start, end) of dictIds."""
+    d = col.dict_values
+    if col.stored_type == STRING:
+        keys = [_java_key(x) for x in d]
+
+        def ss(v, side):
+            k = _java_key(str(v))
+            return bisect.bisect_left(keys, k) if side == "left" else bisect.bisect_right(keys, k)
+    else:
+        def ss(v, side):
+            return int(np.searchsorted(d, _coerce(v, col.stored_type), side=side))
+    start = 0 if p.lower is None else ss(p.lower, "left" if p.lower_inclusive else "right")
+    end = len(d) if p.upper is None else ss(p.upper, "right" if p.upper_inclusive else "left")
+    return start, max(end, start)
+
+
+def _raw_range(col: ColumnBuffers, p):
+    """*RawValueBasedRangePredicateEvaluator: inclusive bounds, unbounded = type min/max."""
+    t = col.stored_type
+    if t in (INT, LONG):
+        info = np.iinfo(np.int32 if t == INT else np.int64)
+        lo = info.min if p.lower is None else int(p.lower) + (0 if p.lower_inclusive else 1)
+        hi = info.max if p.upper is None else int(p.upper) - (0 if p.upper_inclusive else 1)
+        return lo, hi
+    if t == FLOAT:
+        f = np.float32
+        lo = -math.inf if p.lower is None else float(f(p.lower) if p.lower_inclusive else np.nextafter(f(p.lower), f(np.inf)))
+        hi = math.inf if p.upper is None else float(f(p.upper) if p.upper_inclusive else np.nextafter(f(p.upper), f(-np.inf)))
+        return lo, hi
+    lo = -math.inf if p.lower is None else (float(p.lower) if p.lower_inclusive else float(np.nextafter(float(p.lower), np.inf)))
+    hi = math.inf if p.upper is None else (float(p.upper) if p.upper_inclusive else float(np.nextafter(float(p.upper), -np.inf)))
+    return lo, hi
+
+
+class OracleSegment:
+    """Host view of one segment's buffers in the oracle's column layout."""
+
+    def __init__(self, seg: SegmentBuffers):
+        self.seg = seg
+        self.names = list(seg.columns)
+        self.index = {n: i for i, n in enumerate(self.names)}
+        self._keep = []
+        cols = (OColumn * len(self.names))()
+        for i, n in enumerate(self.names):
+            cb = seg.columns[n]
+            oc = cols[i]
+            oc.encoding = OR_ENC[cb.encoding]
+            oc.stored_type = OR_TYPE.get(cb.stored_type, 0)
+            oc.bits = cb.bits_per_element
+            oc.cardinality = cb.cardinality
+            if cb.encoding == "RAW":
+                h = parse_raw_fwd_header(cb.fwd)
+                buf = np.frombuffer(cb.fwd, dtype=np.uint8)[h.raw_data_start:].copy()
+            else:
+                buf = np.frombuffer(cb.fwd, dtype=np.uint8).copy()
+                buf = np.concatenate([buf, np.zeros(16, np.uint8)])  # reads of the last byte's neighbour
+            self._keep.append(buf)
+            oc.fwd = _ptr(buf)
+            if cb.has_dictionary and cb.stored_type != STRING:
+                dv = np.ascontiguousarray(cb.dict_values)
+                self._keep.append(dv)
+                oc.dict = _ptr(dv)
+        self.cols = cols
+
+    def leaves(self, qc: QueryContext, use_inverted: bool = True):
+        out = []
+        n = self.seg.num_docs
+        for ci, clause in enumerate(qc.cnf):
+            for p, neg in clause:
+                cb = self.seg.columns[p.column]
+                lf = OLeaf()
+                lf.column = self.index[p.column]
+                lf.clause = ci
+                lf.negate = 1 if neg else 0
+                negated_type = p.type in ("NOT_EQ", "NOT_IN")
+                if negated_type:
+                    lf.negate ^= 1
+                if cb.has_dictionary:
+                    if p.type == "RANGE":
+                        s, e = _dict_range(cb, p)
+                        ids = list(range(s, e))
+                    else:
+                        ids = _dict_positions(cb, p.values)
+                    if use_inverted and cb.inverted is not None and p.type != "RANGE":
+                        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+                        idarr = np.array(ids, dtype=np.int32)
+                        inv = np.frombuffer(cb.inverted, dtype=np.uint8)
+                        rc = lib().oracle_inverted_to_bitset(_ptr(inv), cb.cardinality, _ptr(idarr), len(ids),
+                                                             _ptr(bits), n)
+                        assert rc == 0, rc
+                        self._keep += [bits, idarr, inv]
+                        lf.kind = DOC_BITSET
+                        lf.doc_bitset = _ptr(bits)
+                    elif p.type == "RANGE":
+                        lf.kind = DICT_RANGE
+                        lf.lo_i, lf.hi_i = ids[0] if ids else 0, (ids[-1] + 1) if ids else 0
+                    else:
+                        mask = np.zeros(cb.cardinality + 1, dtype=np.uint8)
+                        mask[ids] = 1
+                        self._keep.append(mask)
+                        lf.kind = DICT_SET
+                        lf.dict_mask = _ptr(mask)
+                else:
+                    if p.type == "RANGE":
+                        lf.kind = RAW_RANGE
+                        lo, hi = _raw_range(cb, p)
+                        if cb.stored_type in (INT, LONG):
+                            lf.lo_i, lf.hi_i = lo, hi
+                        else:
+                            lf.lo_d, lf.hi_d = lo, hi
+                    else:
+                        lf.kind = RAW_IN
+                        if cb.stored_type in (INT, LONG):
+                            arr = np.array([int(v) for v in p.values], dtype=np.int64)
+                            lf.set_i = _ptr(arr)
+                        else:
+                            arr = np.array([float(np.float32(v)) if cb.stored_type == FLOAT else float(v)
+                                            for v in p.values], dtype=np.float64)
+                            lf.set_d = _ptr(arr)
+                        lf.set_n = len(arr)
+                        self._keep.append(arr)
+                out.append(lf)
+        arr = (OLeaf * max(len(out), 1))(*out)
+        return arr, len(out)
+
+    def filter_bitset(self, qc: QueryContext, use_inverted: bool = True):
+        n = self.seg.num_docs
+        bits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+        leaves, nl = self.leaves(qc, use_inverted)
+        cnt = lib().oracle_filter(self.cols, n, leaves, nl, _ptr(bits))
+        return bits, int(cnt)
+
+    def key_values(self, dict_ids, group_by: Sequence[str]) -> tuple:
+        out = []
+        for g, d in zip(group_by, dict_ids):
+            cb = self.seg.columns[g]
+            v = cb.dict_values[int(d)]
+            out.append(v if cb.stored_type == STRING else (float(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
+        return tuple(out)
+
+
+def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True):
+    """Run a query over segments on the CPU oracle: returns (num_docs_matched, groups) where groups
+    maps key tuple -> intermediate results per aggregation (AVG as (sum, count)), combined across
+    segments with AggregationFunction.merge semantics."""
+    qc = parse_sql(query) if isinstance(query, str) else query
+    total = 0
+    groups: Dict[tuple, list] = {}
+    for seg in segments:
+        os_ = OracleSegment(seg)
+        if qc.cnf:
+            bits, cnt = os_.filter_bitset(qc, use_inverted)
+        else:
+            bits, cnt = None, seg.num_docs
+        total += cnt
+        # native aggregations: AVG -> SUM + COUNT
+        nat = []
+        slots = []
+        for a in qc.aggregations:
+            if a.func == "AVG":
+                nat.append(("SUM", a.column))
+                nat.append(("COUNT", "*"))
+                slots.append(("avg", len(nat) - 2, len(nat) - 1))
+            else:
+                nat.append((a.func, a.column))
+                slots.append(("direct", len(nat) - 1))
+        if not nat:
+            nat.append(("COUNT", "*"))
+        aggs = (OAgg * len(nat))(*[OAgg(AGG[f], -1 if c == "*" else os_.index[c]) for f, c in nat])
+        bptr = _ptr(bits) if bits is not None else None
+        if qc.group_by:
+            cap = max(cnt, 1)
+            keys = np.zeros(cap * len(qc.group_by), dtype=np.int32)
+            vals = np.zeros(cap * len(nat), dtype=np.float64)
+            vali = np.zeros(cap * len(nat), dtype=np.int64)
+            gcols = np.array([os_.index[g] for g in qc.group_by], dtype=np.int32)
+            ng = lib().oracle_group_by(os_.cols, seg.num_docs, bptr, _ptr(gcols), len(gcols), aggs, len(nat), cap,
+                                       _ptr(keys), _ptr(vals), _ptr(vali))
+            assert ng >= 0, ng
+            seg_groups = {}
+            for g in range(ng):
+                kv = os_.key_values(keys[g * len(qc.group_by):(g + 1) * len(qc.group_by)], qc.group_by)
+                seg_groups[kv] = _parts(qc, slots, nat, vals[g * len(nat):(g + 1) * len(nat)],
+                                        vali[g * len(nat):(g + 1) * len(nat)])
+        else:
+            vals = np.zeros(len(nat), dtype=np.float64)
+            vali = np.zeros(len(nat), dtype=np.int64)
+            lib().oracle_aggregate(os_.cols, seg.num_docs, bptr, aggs, len(nat), _ptr(vals), _ptr(vali))
+            seg_groups = {(): _parts(qc, slots, nat, vals, vali)}
+        for k, parts in seg_groups.items():
+            if k in groups:
+                groups[k] = [merge_partial(a.func, x, y) for a, x, y in zip(qc.aggregations, groups[k], parts)]
+            else:
+                groups[k] = parts
+    return total, groups
+
+
+def _parts(qc, slots, nat, vals, vali):
+    out = []
+    for a, s in zip(qc.aggregations, slots):
+        if s[0] == "avg":
+            out.append((float(vals[s[1]]), int(vali[s[2]])))
+        elif a.func in ("COUNT", "SUMLONG"):
+            out.append(int(vali[s[1]]))
+        else:
+            out.append(float(vals[s[1]]))
+    return out
+
+
+def rows(query, segments, use_inverted: bool = True):
+    qc = parse_sql(query) if isinstance(query, str) else query
+    _, groups = execute(qc, segments, use_inverted)
+    return reduce_rows(qc, groups)

@@ -1,0 +1,547 @@
+/*
+ * pinot_oracle.c — scalar CPU restatement of Pinot's segment scan / filter /
+ * aggregation / group-by hot path. TEST INFRASTRUCTURE ONLY (see pinot_oracle.h).
+ *
+ * Reference paths are relative to the reference checkout root; "PDB" below is
+ * pinot-segment-local/src/main/java/org/apache/pinot/segment/local/io/util/PinotDataBitSet.java.
+ */
+#include "pinot_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ helpers */
+static uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+static uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static uint64_t le64(const uint8_t* p) { return (uint64_t)le32(p) | ((uint64_t)le32(p + 4) << 32); }
+
+/* ------------------------------------------------------------------ forward index */
+
+/* PinotDataBitSet.readInt(int index, int numBitsPerValue) — PDB:80-102.
+ * FixedBitIntReader.BitNReader.read / FixedBitSVForwardIndexReaderV2.getDictId return the
+ * same value (they are unrolled specialisations of this stream layout). */
+int32_t oracle_fixedbit_read(const uint8_t* buf, int32_t bits, int64_t index) {
+  const uint32_t BYTE_MASK = 0xFF;
+  int64_t bit_offset = index * (int64_t)bits;
+  int64_t byte_offset = bit_offset / 8;
+  int bit_in_first = (int)(bit_offset % 8);
+  uint32_t current = buf[byte_offset] & (BYTE_MASK >> bit_in_first);
+  int left = bits - (8 - bit_in_first);
+  if (left <= 0) {
+    return (int32_t)(current >> -left);
+  }
+  while (left > 8) {
+    byte_offset++;
+    current = (current << 8) | (buf[byte_offset] & BYTE_MASK);
+    left -= 8;
+  }
+  return (int32_t)((current << left) | ((buf[byte_offset + 1] & BYTE_MASK) >> (8 - left)));
+}
+
+/* PinotDataBitSet.readInt(int startIndex, int numBitsPerValue, int length, int[] buffer) — PDB:104-141 */
+void oracle_fixedbit_read_range(const uint8_t* buf, int32_t bits, int64_t start, int64_t n, int32_t* out) {
+  for (int64_t i = 0; i < n; i++) out[i] = oracle_fixedbit_read(buf, bits, start + i);
+}
+
+/* PinotDataBitSet.writeInt(int index, int numBitsPerValue, int value) — PDB:143-170 */
+void oracle_fixedbit_write(uint8_t* buf, int32_t bits, int64_t start, int64_t n, const int32_t* values) {
+  for (int64_t k = 0; k < n; k++) {
+    uint32_t value = (uint32_t)values[k];
+    int64_t bit_offset = (start + k) * (int64_t)bits;
+    int64_t byte_offset = bit_offset / 8;
+    int bit_in_first = (int)(bit_offset % 8);
+    uint32_t first = buf[byte_offset];
+    uint32_t first_mask = 0xFFu >> bit_in_first;
+    int left = bits - (8 - bit_in_first);
+    if (left <= 0) {
+      first_mask &= (0xFFu << -left) & 0xFFu;
+      buf[byte_offset] = (uint8_t)((first & ~first_mask) | (value << -left));
+    } else {
+      buf[byte_offset] = (uint8_t)((first & ~first_mask) | ((value >> left) & first_mask));
+      while (left > 8) {
+        left -= 8;
+        byte_offset++;
+        buf[byte_offset] = (uint8_t)(value >> left);
+      }
+      byte_offset++;
+      uint32_t last = buf[byte_offset];
+      buf[byte_offset] = (uint8_t)((last & (0xFFu >> left)) | (value << (8 - left)));
+    }
+  }
+}
+
+/* SortedIndexReaderImpl.getDictId: binary search over (min,max) pairs
+ * (pinot-segment-local/.../readers/sorted/SortedIndexReaderImpl.java:50-100). */
+int32_t oracle_sorted_dict_id(const uint8_t* pairs, int32_t cardinality, int64_t doc) {
+  int32_t lo = 0, hi = cardinality - 1;
+  while (lo <= hi) {
+    int32_t mid = (lo + hi) >> 1;
+    int64_t start = (int32_t)be32(pairs + 8 * (int64_t)mid);
+    if (start <= doc) {
+      lo = mid + 1;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  return hi;
+}
+
+/* FixedBytePower2ChunkSVForwardIndexReader.getInt/getLong/getFloat/getDouble on a
+ * PASS_THROUGH buffer: _rawData.getX(docId * size), big-endian
+ * (.../readers/forward/FixedBytePower2ChunkSVForwardIndexReader.java:48-90). */
+int64_t oracle_raw_read_i64(const uint8_t* raw, int32_t type, int64_t index) {
+  switch (type) {
+    case OR_INT: return (int32_t)be32(raw + 4 * index);
+    case OR_LONG: return (int64_t)be64(raw + 8 * index);
+    default: return 0;
+  }
+}
+double oracle_raw_read_f64(const uint8_t* raw, int32_t type, int64_t index) {
+  switch (type) {
+    case OR_INT: return (double)(int32_t)be32(raw + 4 * index);
+    case OR_LONG: return (double)(int64_t)be64(raw + 8 * index);
+    case OR_FLOAT: {
+      uint32_t u = be32(raw + 4 * index);
+      float f;
+      memcpy(&f, &u, 4);
+      return (double)f;
+    }
+    case OR_DOUBLE: {
+      uint64_t u = be64(raw + 8 * index);
+      double d;
+      memcpy(&d, &u, 8);
+      return d;
+    }
+    default: return 0.0;
+  }
+}
+
+static int32_t dict_id_of(const oracle_column* c, int64_t doc) {
+  if (c->encoding == OR_ENC_SORTED) return oracle_sorted_dict_id(c->fwd, c->cardinality, doc);
+  return oracle_fixedbit_read(c->fwd, c->bits, doc);
+}
+
+void oracle_column_dict_ids(const oracle_column* col, int64_t start, int64_t n, int32_t* out) {
+  for (int64_t i = 0; i < n; i++) out[i] = dict_id_of(col, start + i);
+}
+
+/* value of a column at doc as the stored type: dictionary lookup for dict columns
+ * (Dictionary.readIntValues etc. behind BlockValSet.getXValuesSV) or raw read. */
+static int is_float_type(int t) { return t == OR_FLOAT || t == OR_DOUBLE; }
+
+static int64_t value_i64(const oracle_column* c, int64_t doc) {
+  if (c->encoding == OR_ENC_RAW) return oracle_raw_read_i64(c->fwd, c->stored_type, doc);
+  int32_t id = dict_id_of(c, doc);
+  if (c->stored_type == OR_INT) return ((const int32_t*)c->dict)[id];
+  return ((const int64_t*)c->dict)[id];
+}
+static double value_f64(const oracle_column* c, int64_t doc) {
+  if (c->encoding == OR_ENC_RAW) return oracle_raw_read_f64(c->fwd, c->stored_type, doc);
+  int32_t id = dict_id_of(c, doc);
+  switch (c->stored_type) {
+    case OR_INT: return (double)((const int32_t*)c->dict)[id];
+    case OR_LONG: return (double)((const int64_t*)c->dict)[id];
+    case OR_FLOAT: return (double)((const float*)c->dict)[id];
+    default: return ((const double*)c->dict)[id];
+  }
+}
+
+/* ------------------------------------------------------------------ roaring */
+
+/* RoaringBitmap 1.6.14 portable deserialisation (org.roaringbitmap.buffer.ImmutableRoaringBitmap,
+ * third-party, not vendored): cookie 12346 = no run containers (int32 size follows),
+ * 12347 | (size-1)<<16 = with run-container bitset; then (key u16, card-1 u16) per container;
+ * offsets (int32) present unless (has runs && size < 4); then array (u16 x card), bitmap
+ * (u64 x 1024) or run (nruns u16 + (start,len-1) u16 pairs) containers. Little-endian. */
+int oracle_roaring_to_bitset(const uint8_t* buf, int64_t len, uint64_t* bitset, int64_t num_docs) {
+  if (len < 4) return -1;
+  uint32_t cookie = le32(buf);
+  int64_t pos = 4;
+  int32_t size;
+  const uint8_t* runbits = NULL;
+  int has_run = 0;
+  if ((cookie & 0xFFFF) == 12347) {
+    has_run = 1;
+    size = (int32_t)(cookie >> 16) + 1;
+    runbits = buf + pos;
+    pos += (size + 7) / 8;
+  } else if (cookie == 12346) {
+    size = (int32_t)le32(buf + pos);
+    pos += 4;
+  } else {
+    return -2;
+  }
+  const uint8_t* header = buf + pos;
+  pos += 4 * (int64_t)size;
+  if (!has_run || size >= 4) pos += 4 * (int64_t)size; /* skip offsets; containers are contiguous */
+  for (int32_t i = 0; i < size; i++) {
+    uint32_t key = le16(header + 4 * i);
+    int32_t card = le16(header + 4 * i + 2) + 1;
+    int64_t base = (int64_t)key << 16;
+    int is_run = has_run && (runbits[i / 8] >> (i % 8)) & 1;
+    if (is_run) {
+      int32_t nruns = le16(buf + pos);
+      pos += 2;
+      for (int32_t r = 0; r < nruns; r++) {
+        int64_t s = le16(buf + pos + 4 * r), l = le16(buf + pos + 4 * r + 2);
+        for (int64_t d = base + s; d <= base + s + l; d++)
+          if (d < num_docs) bitset[d >> 6] |= 1ull << (d & 63);
+      }
+      pos += 4 * (int64_t)nruns;
+    } else if (card <= 4096) {
+      for (int32_t j = 0; j < card; j++) {
+        int64_t d = base + le16(buf + pos + 2 * j);
+        if (d < num_docs) bitset[d >> 6] |= 1ull << (d & 63);
+      }
+      pos += 2 * (int64_t)card;
+    } else {
+      for (int32_t w = 0; w < 1024; w++) {
+        uint64_t word = le64(buf + pos + 8 * w);
+        while (word) {
+          int b = __builtin_ctzll(word);
+          int64_t d = base + 64 * w + b;
+          if (d < num_docs) bitset[d >> 6] |= 1ull << (d & 63);
+          word &= word - 1;
+        }
+      }
+      pos += 8192;
+    }
+    if (pos > len) return -3;
+  }
+  return 0;
+}
+
+/* BitmapInvertedIndexReader.getDocIds(dictId) (.../readers/BitmapInvertedIndexReader.java:44-60)
+ * OR-ed over the given dictIds, as BitmapBasedFilterOperator does for EQ/IN
+ * (pinot-core/.../operator/filter/BitmapBasedFilterOperator.java). */
+int oracle_inverted_to_bitset(const uint8_t* inv, int32_t cardinality, const int32_t* dict_ids, int32_t n,
+                              uint64_t* bitset, int64_t num_docs) {
+  uint32_t first = be32(inv);
+  const uint8_t* bitmaps = inv + 4 * ((int64_t)cardinality + 1);
+  for (int32_t k = 0; k < n; k++) {
+    int32_t id = dict_ids[k];
+    if (id < 0 || id >= cardinality) return -1;
+    uint32_t s = be32(inv + 4 * (int64_t)id), e = be32(inv + 4 * ((int64_t)id + 1));
+    int rc = oracle_roaring_to_bitset(bitmaps + (s - first), (int64_t)(e - s), bitset, num_docs);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ filter */
+
+/* One predicate on one doc: PredicateEvaluator.applySV semantics
+ * (RangePredicateEvaluatorFactory.java:221-224 dict range, :416-418 raw int range with
+ * inclusive bounds; InPredicateEvaluatorFactory.java:188-190 dict set). */
+static int leaf_match(const oracle_column* cols, const oracle_leaf* lf, int64_t doc) {
+  int m = 0;
+  switch (lf->kind) {
+    case OR_PRED_DICT_RANGE: {
+      int32_t id = dict_id_of(&cols[lf->column], doc);
+      m = lf->lo_i <= id && lf->hi_i > id;
+      break;
+    }
+    case OR_PRED_DICT_SET: {
+      int32_t id = dict_id_of(&cols[lf->column], doc);
+      m = lf->dict_mask[id] != 0;
+      break;
+    }
+    case OR_PRED_RAW_RANGE: {
+      const oracle_column* c = &cols[lf->column];
+      if (is_float_type(c->stored_type)) {
+        double v = value_f64(c, doc);
+        m = v >= lf->lo_d && v <= lf->hi_d;
+      } else {
+        int64_t v = value_i64(c, doc);
+        m = v >= lf->lo_i && v <= lf->hi_i;
+      }
+      break;
+    }
+    case OR_PRED_RAW_IN: {
+      const oracle_column* c = &cols[lf->column];
+      if (is_float_type(c->stored_type)) {
+        double v = value_f64(c, doc);
+        for (int32_t k = 0; k < lf->set_n && !m; k++) m = lf->set_d[k] == v;
+      } else {
+        int64_t v = value_i64(c, doc);
+        for (int32_t k = 0; k < lf->set_n && !m; k++) m = lf->set_i[k] == v;
+      }
+      break;
+    }
+    case OR_PRED_DOC_BITSET:
+      m = (lf->doc_bitset[doc >> 6] >> (doc & 63)) & 1;
+      break;
+  }
+  return lf->negate ? !m : m;
+}
+
+/* Filter tree in conjunctive normal form, evaluated doc by doc like
+ * ScanBasedFilterOperator/SVScanDocIdIterator (pinot-core/.../dociditerators/SVScanDocIdIterator.java:79-103)
+ * under AndFilterOperator / OrFilterOperator. Returns the number of matching docs. */
+int64_t oracle_filter(const oracle_column* cols, int64_t num_docs, const oracle_leaf* leaves, int32_t nleaves,
+                      uint64_t* out_bitset) {
+  int32_t nclauses = 0;
+  for (int32_t i = 0; i < nleaves; i++)
+    if (leaves[i].clause + 1 > nclauses) nclauses = leaves[i].clause + 1;
+  memset(out_bitset, 0, sizeof(uint64_t) * (size_t)((num_docs + 63) / 64));
+  int64_t count = 0;
+  for (int64_t doc = 0; doc < num_docs; doc++) {
+    int all = 1;
+    for (int32_t c = 0; c < nclauses && all; c++) {
+      int any = 0;
+      for (int32_t i = 0; i < nleaves && !any; i++)
+        if (leaves[i].clause == c) any = leaf_match(cols, &leaves[i], doc);
+      all = any;
+    }
+    if (all) {
+      out_bitset[doc >> 6] |= 1ull << (doc & 63);
+      count++;
+    }
+  }
+  return count;
+}
+
+/* BlockDocIdIterator order: ascending docIds */
+int64_t oracle_bitset_to_doc_ids(const uint64_t* bitset, int64_t num_docs, int32_t* out) {
+  int64_t n = 0;
+  for (int64_t d = 0; d < num_docs; d++)
+    if ((bitset[d >> 6] >> (d & 63)) & 1) out[n++] = (int32_t)d;
+  return n;
+}
+
+/* ------------------------------------------------------------------ aggregation */
+
+#define MAX_DOC_PER_CALL 10000 /* pinot-core/.../plan/DocIdSetPlanNode.java:28 */
+
+/* AggregationOperator over blocks of <= 10000 matching docs
+ * (pinot-core/.../operator/query/AggregationOperator.java, DocIdSetOperator). Per block:
+ * SUM: double innerSum over the block then holder += innerSum (SumAggregationFunction.java:84-136,160-170);
+ * MIN/MAX: Math.min/Math.max of the block extreme into the holder, initial +/-inf
+ * (MinAggregationFunction.java:38,83-135,175-185); COUNT: long; SUMLONG: long wrap
+ * (SumLongAggregationFunction.java). */
+int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset, const oracle_agg* aggs,
+                     int32_t naggs, double* out, int64_t* out_i64) {
+  double* holder = (double*)malloc(sizeof(double) * (size_t)naggs);
+  double* inner = (double*)malloc(sizeof(double) * (size_t)naggs);
+  int64_t* li = (int64_t*)calloc((size_t)naggs, sizeof(int64_t));
+  for (int32_t a = 0; a < naggs; a++) {
+    holder[a] = aggs[a].func == OR_AGG_MIN ? INFINITY : aggs[a].func == OR_AGG_MAX ? -INFINITY : 0.0;
+  }
+  int64_t doc = 0;
+  while (doc < num_docs) {
+    /* gather the next block of up to MAX_DOC_PER_CALL matching docs */
+    int64_t block[MAX_DOC_PER_CALL];
+    int32_t len = 0;
+    while (doc < num_docs && len < MAX_DOC_PER_CALL) {
+      if (!bitset || ((bitset[doc >> 6] >> (doc & 63)) & 1)) block[len++] = doc;
+      doc++;
+    }
+    if (len == 0) break;
+    for (int32_t a = 0; a < naggs; a++) {
+      const oracle_column* c = aggs[a].column >= 0 ? &cols[aggs[a].column] : NULL;
+      switch (aggs[a].func) {
+        case OR_AGG_COUNT:
+          li[a] += len;
+          break;
+        case OR_AGG_SUM: {
+          double s = 0;
+          for (int32_t i = 0; i < len; i++) s += value_f64(c, block[i]);
+          holder[a] = s + holder[a];
+          break;
+        }
+        case OR_AGG_SUMLONG: {
+          uint64_t s = 0;
+          for (int32_t i = 0; i < len; i++) s += (uint64_t)value_i64(c, block[i]);
+          li[a] = (int64_t)((uint64_t)li[a] + s);
+          break;
+        }
+        case OR_AGG_MIN: {
+          double m = INFINITY;
+          for (int32_t i = 0; i < len; i++) m = fmin(m, value_f64(c, block[i]));
+          /* Math.min propagates NaN; fmin does not */
+          for (int32_t i = 0; i < len; i++)
+            if (isnan(value_f64(c, block[i]))) m = NAN;
+          holder[a] = (isnan(m) || isnan(holder[a])) ? NAN : fmin(m, holder[a]);
+          break;
+        }
+        case OR_AGG_MAX: {
+          double m = -INFINITY;
+          for (int32_t i = 0; i < len; i++) m = fmax(m, value_f64(c, block[i]));
+          for (int32_t i = 0; i < len; i++)
+            if (isnan(value_f64(c, block[i]))) m = NAN;
+          holder[a] = (isnan(m) || isnan(holder[a])) ? NAN : fmax(m, holder[a]);
+          break;
+        }
+      }
+    }
+  }
+  for (int32_t a = 0; a < naggs; a++) {
+    if (aggs[a].func == OR_AGG_COUNT || aggs[a].func == OR_AGG_SUMLONG) {
+      out[a] = (double)li[a];
+      out_i64[a] = li[a];
+    } else {
+      out[a] = holder[a];
+      out_i64[a] = 0;
+    }
+  }
+  free(holder);
+  free(inner);
+  free(li);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ group-by */
+
+typedef struct {
+  const int32_t* ids; /* dictIds of the doc's group-by columns */
+  int64_t doc;
+} key_doc;
+
+static int g_ngroup; /* qsort has no context argument */
+
+/* order of DictionaryBasedGroupKeyGenerator raw keys: column n-1 most significant */
+static int cmp_key_doc(const void* a, const void* b) {
+  const key_doc* x = (const key_doc*)a;
+  const key_doc* y = (const key_doc*)b;
+  for (int32_t j = g_ngroup - 1; j >= 0; j--)
+    if (x->ids[j] != y->ids[j]) return x->ids[j] < y->ids[j] ? -1 : 1;
+  return x->doc < y->doc ? -1 : (x->doc > y->doc);
+}
+
+/* DictionaryBasedGroupKeyGenerator raw keys: key = sum_j dictId_j * prod_{i<j} card_i, i.e. the
+ * loop `rawKey = rawKey * card[j] + dictId[j]` for j = n-1..0
+ * (pinot-core/.../aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:316-327,427-434); beyond
+ * the long range the ARRAY_MAP_BASED holder keys on the dictId array itself (same grouping), so the
+ * oracle groups on the dictId tuple and emits it (out_keys[g*ngroup + j]).
+ * Per group, docs are folded in docId order with the group-by semantics of each function:
+ * SUM: holder + value (SumAggregationFunction.java:190-200), MIN: `value < holder`
+ * (MinAggregationFunction.java:215-223), MAX: `value > holder`, COUNT: +1, SUMLONG: long wrap. */
+int64_t oracle_group_by(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset,
+                        const int32_t* group_cols, int32_t ngroup, const oracle_agg* aggs, int32_t naggs,
+                        int64_t max_groups, int32_t* out_keys, double* out_vals, int64_t* out_i64) {
+  /* ARRAY_BASED holder (DictionaryBasedGroupKeyGenerator.java:144-152,304-342): when the raw key
+   * space is at most arrayBasedThreshold (10000), the raw key is the group id — one array slot per
+   * possible key, docs folded in docId order. */
+  double prod = 1;
+  for (int32_t j = 0; j < ngroup; j++) prod *= (double)cols[group_cols[j]].cardinality;
+  if (prod <= 10000) {
+    int64_t nkeys = (int64_t)prod;
+    double* hv = (double*)malloc(sizeof(double) * (size_t)(nkeys * naggs));
+    int64_t* hi = (int64_t*)calloc((size_t)(nkeys * naggs), sizeof(int64_t));
+    int64_t* cnt = (int64_t*)calloc((size_t)nkeys, sizeof(int64_t));
+    for (int64_t k = 0; k < nkeys; k++)
+      for (int32_t a = 0; a < naggs; a++)
+        hv[k * naggs + a] = aggs[a].func == OR_AGG_MIN ? INFINITY : aggs[a].func == OR_AGG_MAX ? -INFINITY : 0.0;
+    for (int64_t d = 0; d < num_docs; d++) {
+      if (bitset && !((bitset[d >> 6] >> (d & 63)) & 1)) continue;
+      int64_t key = 0;
+      for (int32_t j = ngroup - 1; j >= 0; j--) key = key * cols[group_cols[j]].cardinality + dict_id_of(&cols[group_cols[j]], d);
+      cnt[key]++;
+      for (int32_t a = 0; a < naggs; a++) {
+        const oracle_column* c = aggs[a].column >= 0 ? &cols[aggs[a].column] : NULL;
+        double* h = &hv[key * naggs + a];
+        int64_t* li = &hi[key * naggs + a];
+        switch (aggs[a].func) {
+          case OR_AGG_COUNT: *li += 1; *h = (double)*li; break;
+          case OR_AGG_SUM: *h = *h + value_f64(c, d); break;
+          case OR_AGG_SUMLONG: *li = (int64_t)((uint64_t)*li + (uint64_t)value_i64(c, d)); *h = (double)*li; break;
+          case OR_AGG_MIN: { double v = value_f64(c, d); if (v < *h) *h = v; break; }
+          case OR_AGG_MAX: { double v = value_f64(c, d); if (v > *h) *h = v; break; }
+        }
+      }
+    }
+    int64_t g = 0;
+    for (int64_t k = 0; k < nkeys; k++) {
+      if (!cnt[k]) continue;
+      if (g >= max_groups) { g = -1; break; }
+      int64_t rem = k;
+      for (int32_t j = 0; j < ngroup; j++) {
+        out_keys[g * ngroup + j] = (int32_t)(rem % cols[group_cols[j]].cardinality);
+        rem /= cols[group_cols[j]].cardinality;
+      }
+      for (int32_t a = 0; a < naggs; a++) {
+        out_vals[g * naggs + a] = hv[k * naggs + a];
+        out_i64[g * naggs + a] = hi[k * naggs + a];
+      }
+      g++;
+    }
+    free(hv);
+    free(hi);
+    free(cnt);
+    return g;
+  }
+  int64_t nmatch = 0;
+  for (int64_t d = 0; d < num_docs; d++)
+    if (!bitset || ((bitset[d >> 6] >> (d & 63)) & 1)) nmatch++;
+  key_doc* kd = (key_doc*)malloc(sizeof(key_doc) * (size_t)(nmatch ? nmatch : 1));
+  int32_t* ids = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nmatch ? nmatch : 1) * (size_t)(ngroup ? ngroup : 1));
+  int64_t n = 0;
+  for (int64_t d = 0; d < num_docs; d++) {
+    if (bitset && !((bitset[d >> 6] >> (d & 63)) & 1)) continue;
+    int32_t* row = ids + n * ngroup;
+    for (int32_t j = 0; j < ngroup; j++) row[j] = dict_id_of(&cols[group_cols[j]], d);
+    kd[n].ids = row;
+    kd[n].doc = d;
+    n++;
+  }
+  g_ngroup = ngroup;
+  qsort(kd, (size_t)n, sizeof(key_doc), cmp_key_doc);
+  int64_t g = -1;
+  for (int64_t i = 0; i < n; i++) {
+    int newgroup = i == 0;
+    for (int32_t j = 0; j < ngroup && !newgroup; j++) newgroup = kd[i].ids[j] != kd[i - 1].ids[j];
+    if (newgroup) {
+      g++;
+      if (g >= max_groups) {
+        free(kd);
+        free(ids);
+        return -1;
+      }
+      for (int32_t j = 0; j < ngroup; j++) out_keys[g * ngroup + j] = kd[i].ids[j];
+      for (int32_t a = 0; a < naggs; a++) {
+        int f = aggs[a].func;
+        out_vals[g * naggs + a] = f == OR_AGG_MIN ? INFINITY : f == OR_AGG_MAX ? -INFINITY : 0.0;
+        out_i64[g * naggs + a] = 0;
+      }
+    }
+    int64_t doc = kd[i].doc;
+    for (int32_t a = 0; a < naggs; a++) {
+      const oracle_column* c = aggs[a].column >= 0 ? &cols[aggs[a].column] : NULL;
+      double* h = &out_vals[g * naggs + a];
+      int64_t* hi = &out_i64[g * naggs + a];
+      switch (aggs[a].func) {
+        case OR_AGG_COUNT:
+          *hi += 1;
+          *h = (double)*hi;
+          break;
+        case OR_AGG_SUM:
+          *h = *h + value_f64(c, doc);
+          break;
+        case OR_AGG_SUMLONG:
+          *hi = (int64_t)((uint64_t)*hi + (uint64_t)value_i64(c, doc));
+          *h = (double)*hi;
+          break;
+        case OR_AGG_MIN: {
+          double v = value_f64(c, doc);
+          if (v < *h) *h = v;
+          break;
+        }
+        case OR_AGG_MAX: {
+          double v = value_f64(c, doc);
+          if (v > *h) *h = v;
+          break;
+        }
+      }
+    }
+  }
+  free(kd);
+  free(ids);
+  return g + 1;
+}

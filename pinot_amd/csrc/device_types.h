@@ -1,0 +1,81 @@
+// device_types.h — POD descriptors shared by the host planner (host.cpp) and the gfx950
+// kernels (kernels.hip). Everything here is uploaded verbatim to HBM or passed as kernargs.
+#pragma once
+#include <stdint.h>
+
+namespace pamd {
+
+constexpr int kBlock = 256;                         // 4 waves of 64
+constexpr int kDocsPerThread = 4;                   // 4 consecutive docs per lane
+constexpr int kTileDocs = kBlock * kDocsPerThread;  // 1024 docs per block-tile
+constexpr int kMaxSlots = 8;                        // distinct columns referenced by one query
+constexpr int kMaxLeaves = 16;                      // predicate leaves
+constexpr int kMaxClauses = 16;                     // CNF clauses (4 bits each in a 64-bit word)
+constexpr int kMaxAcc = 10;                         // accumulator arrays (acc 0 = COUNT)
+constexpr int kMaxGroupCols = 4;
+// slack the kernels may read past the end of a column buffer (5 dwords of a bit window, a 32 B
+// value vector of the last tile)
+constexpr int kPadBytes = kTileDocs * 8 + 256;
+
+// column encodings (pinot_amd_fwd_encoding)
+enum : int32_t { ENC_FIXED_BIT = 0, ENC_RAW = 1, ENC_SORTED = 2 };
+// value types (pinot_amd_data_type)
+enum : int32_t { T_INT = 0, T_LONG = 1, T_FLOAT = 2, T_DOUBLE = 3, T_STRING = 4 };
+
+// predicate leaf kinds (what a resolved PredicateEvaluator reduces to)
+enum : int32_t {
+  LEAF_DICT_RANGE = 0,  // lo_i <= dictId < hi_i     (SortedDictionaryBasedRangePredicateEvaluator)
+  LEAF_DICT_SET = 1,    // bit dictId of `bits`       (DictionaryBasedIn/Eq..., unsorted range)
+  LEAF_RAW_RANGE_I = 2, // lo_i <= v <= hi_i          (Int/LongRawValueBasedRangePredicateEvaluator)
+  LEAF_RAW_RANGE_F = 3, // lo_d <= v <= hi_d          (Float/DoubleRawValueBasedRangePredicateEvaluator)
+  LEAF_RAW_IN_I = 4,    // v in sorted in_i[0..in_n)  (Int/LongRawValueBasedInPredicateEvaluator)
+  LEAF_RAW_IN_F = 5,    // v in sorted in_d[0..in_n)
+  LEAF_DOC_RANGE = 6,   // lo_i <= docId <= hi_i      (SortedIndexBasedFilterOperator)
+  LEAF_DOC_BITSET = 7,  // bit docId of `bits`        (BitmapBasedFilterOperator over the inverted index)
+  LEAF_CONST = 8        // lo_i != 0                  (alwaysTrue / alwaysFalse evaluators)
+};
+
+// accumulator ops
+enum : int32_t { ACC_COUNT = 0, ACC_SUM_I64 = 1, ACC_SUM_F64 = 2, ACC_MIN = 3, ACC_MAX = 4 };
+
+struct DevColumn {
+  const uint8_t* data;     // FIXED_BIT: BE bit stream | RAW: BE values | SORTED: LE int32 start docId per dictId
+  const void* dict;        // dictionary values, native LE array of the value type (dict columns)
+  const int32_t* remap;    // dictId -> ordinal in the query's merged key space (group-by columns)
+  int32_t enc, type, bits, card;
+};
+
+struct DevLeaf {
+  int32_t slot, kind, negate, clause;
+  int64_t lo_i, hi_i;
+  double lo_d, hi_d;
+  const uint32_t* bits;    // LEAF_DICT_SET: one bit per dictId; LEAF_DOC_BITSET: one bit per docId
+  const int64_t* in_i;
+  const double* in_d;
+  int32_t in_n, pad;
+};
+
+struct DevSegment {
+  int64_t num_docs;
+  int64_t tile_begin;      // first global tile of this segment
+  DevColumn cols[kMaxSlots];
+  DevLeaf leaves[kMaxLeaves];
+};
+
+// Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the
+// kernel's per-slot loop indexes the decoded values with compile-time indices only.
+struct DevQuery {
+  int32_t nsegs, nslots, nleaves, nclauses;
+  int32_t slot_leaf_begin[kMaxSlots + 1];   // leaves of slot s: [begin[s], begin[s+1]); docId leaves after
+  int32_t slotless_leaf_begin, slotless_leaf_end;
+  int32_t slot_acc_begin[kMaxSlots + 1];    // accumulators fed by slot s
+  int64_t slot_group_stride[kMaxSlots];     // > 0: slot is a group-by column with this key stride
+  int32_t nacc;                             // accumulator arrays, acc 0 = COUNT
+  int32_t acc_op[kMaxAcc];
+  int32_t lds_keys;                         // > 0: LDS-privatised table of lds_keys keys
+  int32_t pad0;
+  int64_t num_keys;                         // dense key space (1 for aggregation only)
+  int64_t total_tiles;
+};
+
+}  // namespace pamd

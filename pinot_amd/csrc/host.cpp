@@ -1,0 +1,1295 @@
+// host.cpp — host side of libpinot_amd.so: segment staging into HBM, per-segment predicate
+// resolution (PredicateEvaluatorProvider), query planning for the fused scan kernel, execution
+// over a batch of segments and result extraction. Implements include/pinot_amd.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pinot_amd.h"
+#include "device_types.h"
+
+namespace pamd {
+hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
+                       unsigned long long* d_matched, int grid, hipStream_t st);
+hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st);
+hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
+                                hipStream_t st);
+hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
+hipError_t launch_read_raw(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out, hipStream_t st);
+hipError_t launch_bitset_binop(const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n, int op,
+                               hipStream_t st);
+hipError_t launch_bitset_not(const uint64_t* a, uint64_t* out, int64_t num_docs, hipStream_t st);
+int64_t compact_num_chunks(int64_t num_docs);
+hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* d_chunk_counts, int64_t* d_total,
+                               hipStream_t st);
+hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
+                                 int32_t* out, hipStream_t st);
+hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const int32_t* sel, int32_t nsel,
+                                 int64_t num_docs, uint64_t* bitset, hipStream_t st);
+}  // namespace pamd
+
+using namespace pamd;
+
+// ------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(PINOT_AMD_EHIP, "%s: %s", #expr, hipGetErrorString(e_));   \
+  } while (0)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// device buffers
+// ------------------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  // allocate n bytes + pad (zeroed), copy `src` (len bytes) to the front
+  int alloc_copy(const void* src, size_t len, size_t pad) {
+    n = len + pad;
+    if (hipMalloc(&p, n) != hipSuccess) return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
+    HIP_OK(hipMemset(p, 0, n));
+    if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
+    return 0;
+  }
+  int alloc(size_t len) {
+    n = len;
+    if (hipMalloc(&p, n ? n : 1) != hipSuccess) return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
+    return 0;
+  }
+};
+
+static uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+static uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+static uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Java String.compareTo order (UTF-16 code units); for the BMP this equals code point order,
+// which for valid UTF-8 equals byte order except for supplementary characters. Compare UTF-16.
+static std::u16string to_utf16(const std::string& s) {
+  std::u16string out;
+  size_t i = 0;
+  while (i < s.size()) {
+    uint32_t c = (uint8_t)s[i];
+    int extra = c < 0x80 ? 0 : c < 0xE0 ? 1 : c < 0xF0 ? 2 : 3;
+    if (extra) c &= (0x3F >> extra);
+    for (int k = 1; k <= extra && i + k < s.size(); ++k) c = (c << 6) | ((uint8_t)s[i + k] & 0x3F);
+    i += 1 + extra;
+    if (c >= 0x10000) {
+      c -= 0x10000;
+      out.push_back((char16_t)(0xD800 + (c >> 10)));
+      out.push_back((char16_t)(0xDC00 + (c & 0x3FF)));
+    } else {
+      out.push_back((char16_t)c);
+    }
+  }
+  return out;
+}
+static bool java_less(const std::string& a, const std::string& b) { return to_utf16(a) < to_utf16(b); }
+
+struct RoaringContainerHost {
+  uint32_t key, kind, count, pad;
+  uint64_t offset;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Segment
+// ------------------------------------------------------------------------------------------------
+struct Column {
+  std::string name;
+  int32_t type = 0, enc = 0, card = 0, bits = 0;
+  DevBuf fwd;            // fixed-bit stream | raw values (from rawDataStart) | sorted LE starts
+  DevBuf dict;           // LE dictionary values (numeric)
+  std::vector<int64_t> dict_i;  // host copies for predicate resolution / result keys
+  std::vector<double> dict_d;
+  std::vector<std::string> dict_s;
+  std::vector<int32_t> sorted_start, sorted_end;  // sorted columns
+  // inverted index
+  DevBuf inv;
+  DevBuf inv_conts;
+  std::vector<uint32_t> inv_dir;  // containers of dictId d: [inv_dir[d], inv_dir[d+1])
+  bool has_inv = false;
+};
+
+struct pinot_amd_segment {
+  std::string name;
+  int64_t num_docs = 0;
+  std::map<std::string, std::unique_ptr<Column>> cols;
+  int64_t device_bytes = 0;
+};
+
+static bool is_float(int t) { return t == T_FLOAT || t == T_DOUBLE; }
+static int value_size(int t) { return (t == T_INT || t == T_FLOAT) ? 4 : 8; }
+
+static int decode_dictionary(Column& c, const uint8_t* d, size_t n) {
+  if (c.type == T_STRING) {
+    if (c.card <= 0) return 0;
+    size_t w = n / (size_t)c.card;
+    if (w * (size_t)c.card != n) return fail(PINOT_AMD_EINVAL, "string dictionary size %zu not a multiple of %d", n, c.card);
+    c.dict_s.resize(c.card);
+    for (int i = 0; i < c.card; ++i) {
+      const char* p = (const char*)d + (size_t)i * w;
+      size_t len = w;
+      while (len > 0 && p[len - 1] == '\0') --len;
+      c.dict_s[i].assign(p, len);
+    }
+    return 0;
+  }
+  const int vs = value_size(c.type);
+  if (n < (size_t)c.card * vs) return fail(PINOT_AMD_EINVAL, "dictionary too small for cardinality %d", c.card);
+  std::vector<uint8_t> le((size_t)c.card * vs);
+  for (int i = 0; i < c.card; ++i) {
+    const uint8_t* p = d + (size_t)i * vs;
+    if (vs == 4) {
+      uint32_t u = be32(p);
+      memcpy(&le[(size_t)i * 4], &u, 4);
+      if (c.type == T_INT) {
+        c.dict_i.push_back((int32_t)u);
+      } else {
+        float f;
+        memcpy(&f, &u, 4);
+        c.dict_d.push_back(f);
+      }
+    } else {
+      uint64_t u = be64(p);
+      memcpy(&le[(size_t)i * 8], &u, 8);
+      if (c.type == T_LONG) {
+        c.dict_i.push_back((int64_t)u);
+      } else {
+        double f;
+        memcpy(&f, &u, 8);
+        c.dict_d.push_back(f);
+      }
+    }
+  }
+  return c.dict.alloc_copy(le.data(), le.size(), 64);
+}
+
+// Parse the RoaringBitmap portable format of every bitmap into a container directory (offsets are
+// relative to the staged inverted-index buffer).
+static int build_inverted_directory(Column& c, const uint8_t* inv, size_t n) {
+  std::vector<RoaringContainerHost> conts;
+  c.inv_dir.assign(1, 0);
+  const size_t hdr = 4 * ((size_t)c.card + 1);
+  if (n < hdr) return fail(PINOT_AMD_EINVAL, "inverted index too small");
+  const uint32_t first = be32(inv);
+  for (int d = 0; d < c.card; ++d) {
+    const uint32_t s = be32(inv + 4 * (size_t)d), e = be32(inv + 4 * ((size_t)d + 1));
+    // offsets may be absolute (whole buffer) or relative to the bitmap area
+    // (BitmapInvertedIndexReader.java:36-45): normalise through the first offset
+    const size_t base = hdr + (size_t)(s - first);
+    const size_t len = (size_t)(e - s);
+    if (base + len > n || len < 4) return fail(PINOT_AMD_EINVAL, "bad bitmap %d in inverted index", d);
+    const uint8_t* b = inv + base;
+    const uint32_t cookie = le32(b);
+    size_t pos = 4;
+    int32_t size;
+    const uint8_t* runbits = nullptr;
+    bool has_run = false;
+    if ((cookie & 0xFFFF) == 12347) {
+      has_run = true;
+      size = (int32_t)(cookie >> 16) + 1;
+      runbits = b + pos;
+      pos += (size + 7) / 8;
+    } else if (cookie == 12346) {
+      size = (int32_t)le32(b + pos);
+      pos += 4;
+    } else {
+      return fail(PINOT_AMD_EUNSUPPORTED, "unknown RoaringBitmap cookie %u", cookie);
+    }
+    const uint8_t* header = b + pos;
+    pos += 4 * (size_t)size;
+    if (!has_run || size >= 4) pos += 4 * (size_t)size;
+    for (int32_t i = 0; i < size; ++i) {
+      RoaringContainerHost rc{};
+      rc.key = le16(header + 4 * i);
+      const uint32_t card = (uint32_t)le16(header + 4 * i + 2) + 1;
+      const bool is_run = has_run && ((runbits[i / 8] >> (i % 8)) & 1);
+      rc.offset = base + pos;
+      if (is_run) {
+        rc.kind = 2;
+        rc.count = le16(b + pos);
+        pos += 2 + 4 * (size_t)rc.count;
+      } else if (card <= 4096) {
+        rc.kind = 0;
+        rc.count = card;
+        pos += 2 * (size_t)card;
+      } else {
+        rc.kind = 1;
+        rc.count = card;
+        pos += 8192;
+      }
+      if (pos > len) return fail(PINOT_AMD_EINVAL, "truncated bitmap %d", d);
+      conts.push_back(rc);
+    }
+    c.inv_dir.push_back((uint32_t)conts.size());
+  }
+  int rc = c.inv.alloc_copy(inv, n, 64);
+  if (rc) return rc;
+  rc = c.inv_conts.alloc_copy(conts.data(), conts.size() * sizeof(RoaringContainerHost), 64);
+  if (rc) return rc;
+  c.has_inv = true;
+  return 0;
+}
+
+extern "C" {
+
+int pinot_amd_abi_version(void) { return PINOT_AMD_ABI_VERSION; }
+const char* pinot_amd_last_error(void) { return g_last_error.c_str(); }
+int pinot_amd_set_device(int device) {
+  HIP_OK(hipSetDevice(device));
+  return 0;
+}
+size_t pinot_amd_required_padding(void) { return (size_t)kPadBytes; }
+
+int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segment** out) {
+  if (!out || num_docs < 0) return fail(PINOT_AMD_EINVAL, "segment_create: bad arguments");
+  if (num_docs > (int64_t)std::numeric_limits<int32_t>::max())
+    return fail(PINOT_AMD_EINVAL, "segment_create: %lld docs exceed Pinot's int docId space", (long long)num_docs);
+  auto* s = new pinot_amd_segment();
+  s->name = name ? name : "";
+  s->num_docs = num_docs;
+  *out = s;
+  return 0;
+}
+
+int pinot_amd_segment_destroy(pinot_amd_segment* seg) {
+  delete seg;
+  return 0;
+}
+
+int64_t pinot_amd_segment_num_docs(const pinot_amd_segment* seg) { return seg ? seg->num_docs : -1; }
+int64_t pinot_amd_segment_device_bytes(const pinot_amd_segment* seg) { return seg ? seg->device_bytes : -1; }
+
+const void* pinot_amd_segment_column_fwd(const pinot_amd_segment* seg, const char* column) {
+  if (!seg || !column) return nullptr;
+  auto it = seg->cols.find(column);
+  return it == seg->cols.end() ? nullptr : it->second->fwd.p;
+}
+
+int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_spec* spec) {
+  if (!seg || !spec || !spec->name) return fail(PINOT_AMD_EINVAL, "add_column: bad arguments");
+  if (seg->cols.count(spec->name)) return fail(PINOT_AMD_EINVAL, "add_column: duplicate column %s", spec->name);
+  auto c = std::make_unique<Column>();
+  c->name = spec->name;
+  c->type = spec->stored_type;
+  c->enc = spec->encoding;
+  c->card = spec->cardinality;
+  c->bits = spec->bits_per_element;
+  const int64_t nd = seg->num_docs;
+  const uint8_t* fwd = (const uint8_t*)spec->h_fwd;
+  if (c->type < T_INT || c->type > T_STRING) return fail(PINOT_AMD_EINVAL, "column %s: bad type", spec->name);
+  int rc = 0;
+  switch (c->enc) {
+    case ENC_FIXED_BIT: {
+      if (c->bits < 1 || c->bits > 31) return fail(PINOT_AMD_EINVAL, "column %s: bitsPerElement %d", spec->name, c->bits);
+      const size_t need = (size_t)((nd * c->bits + 7) / 8);
+      if (spec->fwd_size < need)
+        return fail(PINOT_AMD_EINVAL, "column %s: fixed-bit buffer %zu < %zu bytes", spec->name, spec->fwd_size, need);
+      rc = c->fwd.alloc_copy(fwd, need, kPadBytes);
+      break;
+    }
+    case ENC_SORTED: {
+      if ((size_t)c->card * 8 > spec->fwd_size) return fail(PINOT_AMD_EINVAL, "column %s: sorted index too small", spec->name);
+      c->sorted_start.resize(c->card);
+      c->sorted_end.resize(c->card);
+      for (int i = 0; i < c->card; ++i) {
+        c->sorted_start[i] = (int32_t)be32(fwd + 8 * (size_t)i);
+        c->sorted_end[i] = (int32_t)be32(fwd + 8 * (size_t)i + 4);
+      }
+      rc = c->fwd.alloc_copy(c->sorted_start.data(), c->sorted_start.size() * 4, 64);
+      break;
+    }
+    case ENC_RAW: {
+      if (c->type == T_STRING) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw STRING", spec->name);
+      if (spec->fwd_size < 28) return fail(PINOT_AMD_EINVAL, "column %s: raw index header truncated", spec->name);
+      // BaseChunkForwardIndexReader.java:60-105
+      const int32_t version = (int32_t)be32(fwd), num_chunks = (int32_t)be32(fwd + 4);
+      const int32_t size = (int32_t)be32(fwd + 12);
+      if (version < 2) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw index v%d (SNAPPY)", spec->name, version);
+      const int32_t comp = (int32_t)be32(fwd + 20), dhs = (int32_t)be32(fwd + 24);
+      if (comp != 0)
+        return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d (only PASS_THROUGH is staged)", spec->name,
+                    comp);
+      if (size != value_size(c->type)) return fail(PINOT_AMD_EINVAL, "column %s: entry size %d", spec->name, size);
+      const size_t raw_start = (size_t)dhs + (size_t)num_chunks * (version <= 2 ? 4 : 8);
+      const size_t need = (size_t)nd * size;
+      if (spec->fwd_size < raw_start + need) return fail(PINOT_AMD_EINVAL, "column %s: raw data truncated", spec->name);
+      rc = c->fwd.alloc_copy(fwd + raw_start, need, kPadBytes);
+      break;
+    }
+    default:
+      return fail(PINOT_AMD_EINVAL, "column %s: bad encoding %d", spec->name, c->enc);
+  }
+  if (rc) return rc;
+  if (c->enc != ENC_RAW) {
+    if (!spec->h_dictionary) return fail(PINOT_AMD_EINVAL, "column %s: dictionary required", spec->name);
+    rc = decode_dictionary(*c, (const uint8_t*)spec->h_dictionary, spec->dictionary_size);
+    if (rc) return rc;
+  }
+  if (spec->h_inverted && spec->inverted_size) {
+    if (c->enc == ENC_RAW) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: inverted index on raw column", spec->name);
+    rc = build_inverted_directory(*c, (const uint8_t*)spec->h_inverted, spec->inverted_size);
+    if (rc) return rc;
+  }
+  seg->device_bytes += (int64_t)(c->fwd.n + c->dict.n + c->inv.n + c->inv_conts.n);
+  seg->cols[c->name] = std::move(c);
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// low-level operators
+// ------------------------------------------------------------------------------------------------
+int pinot_amd_fwd_read_dict_ids(const void* d_packed, int32_t bits, int64_t start_doc, int64_t length, int32_t* d_out,
+                                void* stream) {
+  if (!d_packed || !d_out || bits < 1 || bits > 31 || start_doc < 0 || length < 0)
+    return fail(PINOT_AMD_EINVAL, "fwd_read_dict_ids: bad arguments");
+  if (length == 0) return 0;
+  HIP_OK(launch_read_dict_ids((const uint8_t*)d_packed, bits, start_doc, length, d_out, (hipStream_t)stream));
+  return 0;
+}
+
+int pinot_amd_fwd_pack_dict_ids(const int32_t* d_values, int64_t num_values, int32_t bits, void* d_packed,
+                                void* stream) {
+  if (!d_values || !d_packed || bits < 1 || bits > 31 || num_values < 0)
+    return fail(PINOT_AMD_EINVAL, "fwd_pack_dict_ids: bad arguments");
+  if (num_values == 0) return 0;
+  HIP_OK(launch_pack_dict_ids(d_values, num_values, bits, (uint8_t*)d_packed, (hipStream_t)stream));
+  return 0;
+}
+
+int pinot_amd_fwd_read_raw(const void* d_raw, int32_t stored_type, int64_t start_doc, int64_t length, void* d_out,
+                           void* stream) {
+  if (!d_raw || !d_out || stored_type < T_INT || stored_type > T_DOUBLE || start_doc < 0 || length < 0)
+    return fail(PINOT_AMD_EINVAL, "fwd_read_raw: bad arguments");
+  if (length == 0) return 0;
+  HIP_OK(launch_read_raw((const uint8_t*)d_raw, stored_type, start_doc, length, (uint8_t*)d_out, (hipStream_t)stream));
+  return 0;
+}
+
+int pinot_amd_bitset_and(const uint64_t* d_a, const uint64_t* d_b, uint64_t* d_out, int64_t num_words, void* stream) {
+  if (!d_a || !d_b || !d_out || num_words < 0) return fail(PINOT_AMD_EINVAL, "bitset_and: bad arguments");
+  if (num_words == 0) return 0;
+  HIP_OK(launch_bitset_binop(d_a, d_b, d_out, num_words, 0, (hipStream_t)stream));
+  return 0;
+}
+
+int pinot_amd_bitset_or(const uint64_t* d_a, const uint64_t* d_b, uint64_t* d_out, int64_t num_words, void* stream) {
+  if (!d_a || !d_b || !d_out || num_words < 0) return fail(PINOT_AMD_EINVAL, "bitset_or: bad arguments");
+  if (num_words == 0) return 0;
+  HIP_OK(launch_bitset_binop(d_a, d_b, d_out, num_words, 1, (hipStream_t)stream));
+  return 0;
+}
+
+int pinot_amd_bitset_not(const uint64_t* d_a, uint64_t* d_out, int64_t num_docs, void* stream) {
+  if (!d_a || !d_out || num_docs < 0) return fail(PINOT_AMD_EINVAL, "bitset_not: bad arguments");
+  if (num_docs == 0) return 0;
+  HIP_OK(launch_bitset_not(d_a, d_out, num_docs, (hipStream_t)stream));
+  return 0;
+}
+
+static int bitset_count_impl(const uint64_t* d_bitset, int64_t num_docs, DevBuf& counts, DevBuf& total,
+                             int64_t* h_count, hipStream_t st) {
+  const int64_t nc = compact_num_chunks(num_docs);
+  int rc = counts.alloc((size_t)nc * 8);
+  if (rc) return rc;
+  rc = total.alloc(8);
+  if (rc) return rc;
+  HIP_OK(launch_bitset_count(d_bitset, num_docs, (int64_t*)counts.p, (int64_t*)total.p, st));
+  HIP_OK(hipMemcpyAsync(h_count, total.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int pinot_amd_bitset_count(const uint64_t* d_bitset, int64_t num_docs, int64_t* h_count, void* stream) {
+  if (!d_bitset || !h_count || num_docs < 0) return fail(PINOT_AMD_EINVAL, "bitset_count: bad arguments");
+  if (num_docs == 0) {
+    *h_count = 0;
+    return 0;
+  }
+  DevBuf counts, total;
+  return bitset_count_impl(d_bitset, num_docs, counts, total, h_count, (hipStream_t)stream);
+}
+
+int pinot_amd_bitset_to_doc_ids(const uint64_t* d_bitset, int64_t num_docs, int32_t* d_out, int64_t* h_count,
+                                void* stream) {
+  if (!d_bitset || !d_out || !h_count || num_docs < 0) return fail(PINOT_AMD_EINVAL, "bitset_to_doc_ids: bad arguments");
+  if (num_docs == 0) {
+    *h_count = 0;
+    return 0;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  DevBuf counts, total;
+  int rc = bitset_count_impl(d_bitset, num_docs, counts, total, h_count, st);
+  if (rc) return rc;
+  HIP_OK(launch_bitset_compact(d_bitset, num_docs, (const int64_t*)counts.p, d_out, st));
+  HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Query
+// ------------------------------------------------------------------------------------------------
+struct PredSpec {
+  std::string column;
+  int32_t type = 0, clause = 0, negate = 0, use_inv = 0;
+  std::vector<int64_t> vi;
+  std::vector<double> vd;
+  std::vector<std::string> vs;
+  int32_t lower_unbounded = 1, upper_unbounded = 1, lower_inclusive = 1, upper_inclusive = 1;
+  int64_t lower_i = 0, upper_i = 0;
+  double lower_d = 0, upper_d = 0;
+  std::string lower_s, upper_s;
+};
+
+struct AggSpec {
+  int32_t type;
+  std::string column;  // empty for COUNT(*)
+};
+
+struct pinot_amd_query {
+  std::vector<PredSpec> preds;
+  std::vector<std::string> group_by;
+  std::vector<AggSpec> aggs;
+  int64_t num_groups_limit = 100000;
+};
+
+extern "C" {
+
+int pinot_amd_query_create(pinot_amd_query** out) {
+  if (!out) return fail(PINOT_AMD_EINVAL, "query_create: null out");
+  *out = new pinot_amd_query();
+  return 0;
+}
+int pinot_amd_query_destroy(pinot_amd_query* q) {
+  delete q;
+  return 0;
+}
+
+int pinot_amd_query_add_predicate(pinot_amd_query* q, int32_t clause, const pinot_amd_predicate_spec* p,
+                                  int32_t negate) {
+  if (!q || !p || !p->column) return fail(PINOT_AMD_EINVAL, "add_predicate: bad arguments");
+  if (clause < 0 || clause >= kMaxClauses) return fail(PINOT_AMD_EUNSUPPORTED, "add_predicate: clause %d", clause);
+  if (q->preds.size() >= (size_t)kMaxLeaves) return fail(PINOT_AMD_EUNSUPPORTED, "add_predicate: too many predicates");
+  PredSpec s;
+  s.column = p->column;
+  s.type = p->type;
+  s.clause = clause;
+  s.negate = negate ? 1 : 0;
+  s.use_inv = p->use_inverted_index;
+  if (p->type < PINOT_AMD_EQ || p->type > PINOT_AMD_RANGE) return fail(PINOT_AMD_EINVAL, "add_predicate: bad type");
+  if (p->type != PINOT_AMD_RANGE) {
+    if (p->num_values < 1) return fail(PINOT_AMD_EINVAL, "add_predicate: no values");
+    if ((p->type == PINOT_AMD_EQ || p->type == PINOT_AMD_NOT_EQ) && p->num_values != 1)
+      return fail(PINOT_AMD_EINVAL, "add_predicate: EQ takes one value");
+    for (int i = 0; i < p->num_values; ++i) {
+      if (p->h_values_i) s.vi.push_back(p->h_values_i[i]);
+      if (p->h_values_d) s.vd.push_back(p->h_values_d[i]);
+      if (p->h_values_s) s.vs.push_back(p->h_values_s[i] ? p->h_values_s[i] : "");
+    }
+  } else {
+    s.lower_unbounded = p->lower_unbounded;
+    s.upper_unbounded = p->upper_unbounded;
+    s.lower_inclusive = p->lower_inclusive;
+    s.upper_inclusive = p->upper_inclusive;
+    s.lower_i = p->lower_i;
+    s.upper_i = p->upper_i;
+    s.lower_d = p->lower_d;
+    s.upper_d = p->upper_d;
+    if (p->lower_s) s.lower_s = p->lower_s;
+    if (p->upper_s) s.upper_s = p->upper_s;
+  }
+  q->preds.push_back(std::move(s));
+  return 0;
+}
+
+int pinot_amd_query_add_group_by(pinot_amd_query* q, const char* column) {
+  if (!q || !column) return fail(PINOT_AMD_EINVAL, "add_group_by: bad arguments");
+  if (q->group_by.size() >= (size_t)kMaxGroupCols) return fail(PINOT_AMD_EUNSUPPORTED, "add_group_by: too many columns");
+  q->group_by.push_back(column);
+  return 0;
+}
+
+int pinot_amd_query_add_aggregation(pinot_amd_query* q, int32_t agg_type, const char* column, int32_t* out_index) {
+  if (!q) return fail(PINOT_AMD_EINVAL, "add_aggregation: null query");
+  if (agg_type < PINOT_AMD_AGG_COUNT || agg_type > PINOT_AMD_AGG_AVG)
+    return fail(PINOT_AMD_EINVAL, "add_aggregation: bad type");
+  AggSpec a{agg_type, (column && strcmp(column, "*") != 0) ? column : ""};
+  if (agg_type != PINOT_AMD_AGG_COUNT && a.column.empty()) return fail(PINOT_AMD_EINVAL, "add_aggregation: column required");
+  if (out_index) *out_index = (int32_t)q->aggs.size();
+  q->aggs.push_back(a);
+  return 0;
+}
+
+int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit) {
+  if (!q || limit < 1) return fail(PINOT_AMD_EINVAL, "set_num_groups_limit: bad arguments");
+  q->num_groups_limit = limit;
+  return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Result / compiled plan
+// ------------------------------------------------------------------------------------------------
+struct MergedKeyColumn {
+  int32_t type = 0;
+  std::vector<int64_t> vi;
+  std::vector<double> vd;
+  std::vector<std::string> vs;
+  size_t size() const { return type == T_STRING ? vs.size() : is_float(type) ? vd.size() : vi.size(); }
+};
+
+struct pinot_amd_result {
+  hipStream_t stream = nullptr;
+  // compiled plan
+  DevQuery q{};
+  std::vector<DevSegment> hsegs;
+  DevBuf d_segs;
+  std::vector<std::unique_ptr<DevBuf>> owned;  // leaf sets, remaps, bitsets
+  // inverted index leaves to (re)build each execution: (segment, leaf, container selection)
+  struct InvLeaf {
+    int seg;
+    const Column* col;
+    DevBuf* bitset;
+    DevBuf* sel;
+    int32_t nsel;
+    int64_t num_docs;
+  };
+  std::vector<InvLeaf> inv_leaves;
+  int grid = 1;
+  DevBuf acc;
+  DevBuf matched;
+  std::vector<MergedKeyColumn> keys;  // merged dictionaries of the group-by columns
+  std::vector<int64_t> key_stride;
+  std::vector<int32_t> agg_acc;        // aggregation -> accumulator index (AVG: sum acc)
+  std::vector<int32_t> agg_type;
+  int32_t num_group_by = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0;
+  ~pinot_amd_result() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+  }
+};
+
+namespace {
+
+// Dictionary.insertionIndexOf: index if found, else -(insertionPoint + 1)
+template <typename T, typename Less>
+int64_t insertion_index_of(const std::vector<T>& v, const T& x, Less less) {
+  auto it = std::lower_bound(v.begin(), v.end(), x, less);
+  const int64_t i = it - v.begin();
+  if (it != v.end() && !less(x, *it)) return i;
+  return -(i + 1);
+}
+
+struct DictView {
+  const Column* c;
+  int64_t card() const { return c->card; }
+  // insertion index of a predicate value given as int64 / double / string
+  int64_t ins_i(int64_t x) const {
+    if (c->type == T_STRING) return ins_s(std::to_string(x));
+    if (is_float(c->type)) return ins_d((double)x);
+    return insertion_index_of(c->dict_i, x, std::less<int64_t>());
+  }
+  int64_t ins_d(double x) const {
+    if (!is_float(c->type)) {
+      // integer dictionary probed with a double bound: position among integers
+      const double f = std::floor(x);
+      auto it = std::lower_bound(c->dict_i.begin(), c->dict_i.end(), x,
+                                 [](int64_t a, double b) { return (double)a < b; });
+      const int64_t i = it - c->dict_i.begin();
+      if (f == x && it != c->dict_i.end() && (double)*it == x) return i;
+      return -(i + 1);
+    }
+    return insertion_index_of(c->dict_d, x, [](double a, double b) { return a < b; });
+  }
+  int64_t ins_s(const std::string& x) const {
+    if (c->type != T_STRING) {
+      char* end = nullptr;
+      if (is_float(c->type)) return ins_d(strtod(x.c_str(), &end));
+      return insertion_index_of(c->dict_i, (int64_t)strtoll(x.c_str(), &end, 10), std::less<int64_t>());
+    }
+    return insertion_index_of(c->dict_s, x, java_less);
+  }
+};
+
+// dictIds of an EQ/IN predicate's values (PredicateUtils.getDictIdSet): values absent from the
+// dictionary are dropped
+static std::vector<int32_t> dict_ids_of_values(const PredSpec& p, const Column& c) {
+  DictView dv{&c};
+  std::vector<int32_t> ids;
+  const size_t n = std::max(p.vi.size(), std::max(p.vd.size(), p.vs.size()));
+  for (size_t i = 0; i < n; ++i) {
+    int64_t r;
+    if (c.type == T_STRING)
+      r = !p.vs.empty() ? dv.ins_s(p.vs[i]) : dv.ins_i(p.vi[i]);
+    else if (is_float(c.type))
+      r = !p.vd.empty() ? dv.ins_d(p.vd[i]) : !p.vi.empty() ? dv.ins_d((double)p.vi[i]) : dv.ins_s(p.vs[i]);
+    else
+      r = !p.vi.empty() ? dv.ins_i(p.vi[i]) : !p.vd.empty() ? dv.ins_d(p.vd[i]) : dv.ins_s(p.vs[i]);
+    if (r >= 0) ids.push_back((int32_t)r);
+  }
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  return ids;
+}
+
+// SortedDictionaryBasedRangePredicateEvaluator (RangePredicateEvaluatorFactory.java:115-160):
+// [start, end) dictIds
+static void dict_range_of(const PredSpec& p, const Column& c, int64_t* start, int64_t* end) {
+  DictView dv{&c};
+  auto ins = [&](bool lower) -> int64_t {
+    if (c.type == T_STRING) return dv.ins_s(lower ? p.lower_s : p.upper_s);
+    if (is_float(c.type)) return dv.ins_d(lower ? p.lower_d : p.upper_d);
+    return dv.ins_i(lower ? p.lower_i : p.upper_i);
+  };
+  if (p.lower_unbounded) {
+    *start = 0;
+  } else {
+    const int64_t i = ins(true);
+    *start = i < 0 ? -(i + 1) : (p.lower_inclusive ? i : i + 1);
+  }
+  if (p.upper_unbounded) {
+    *end = c.card;
+  } else {
+    const int64_t i = ins(false);
+    *end = i < 0 ? -(i + 1) : (p.upper_inclusive ? i + 1 : i);
+  }
+}
+
+}  // namespace
+
+static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_segment* seg, const PredSpec& p,
+                                 const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st) {
+  memset(L, 0, sizeof(*L));
+  L->slot = slot;
+  L->clause = p.clause;
+  L->negate = p.negate;
+  *needs_slot = true;
+  const bool negated_type = p.type == PINOT_AMD_NOT_EQ || p.type == PINOT_AMD_NOT_IN;
+  if (negated_type) L->negate ^= 1;
+
+  if (c.enc == ENC_RAW) {
+    // raw-value based evaluators
+    if (p.type == PINOT_AMD_RANGE) {
+      if (is_float(c.type)) {
+        L->kind = LEAF_RAW_RANGE_F;
+        double lo = -INFINITY, hi = INFINITY;
+        if (c.type == T_FLOAT) {
+          // FloatRawValueBasedRangePredicateEvaluator: Math.nextUp/nextDown in float
+          if (!p.lower_unbounded) lo = p.lower_inclusive ? (double)(float)p.lower_d : (double)std::nextafter((float)p.lower_d, INFINITY);
+          if (!p.upper_unbounded) hi = p.upper_inclusive ? (double)(float)p.upper_d : (double)std::nextafter((float)p.upper_d, -INFINITY);
+        } else {
+          if (!p.lower_unbounded) lo = p.lower_inclusive ? p.lower_d : std::nextafter(p.lower_d, INFINITY);
+          if (!p.upper_unbounded) hi = p.upper_inclusive ? p.upper_d : std::nextafter(p.upper_d, -INFINITY);
+        }
+        L->lo_d = lo;
+        L->hi_d = hi;
+      } else {
+        // Int/LongRawValueBasedRangePredicateEvaluator: exclusive bounds +/- 1, unbounded = type min/max
+        const int64_t tmin = c.type == T_INT ? INT32_MIN : INT64_MIN, tmax = c.type == T_INT ? INT32_MAX : INT64_MAX;
+        int64_t lo = tmin, hi = tmax;
+        if (!p.lower_unbounded) {
+          if (!p.lower_inclusive && p.lower_i == tmax) return fail(PINOT_AMD_EINVAL, "Invalid range on %s", c.name.c_str());
+          lo = p.lower_inclusive ? p.lower_i : p.lower_i + 1;
+        }
+        if (!p.upper_unbounded) {
+          if (!p.upper_inclusive && p.upper_i == tmin) return fail(PINOT_AMD_EINVAL, "Invalid range on %s", c.name.c_str());
+          hi = p.upper_inclusive ? p.upper_i : p.upper_i - 1;
+        }
+        L->kind = LEAF_RAW_RANGE_I;
+        L->lo_i = lo;
+        L->hi_i = hi;
+      }
+      return 0;
+    }
+    // EQ/NOT_EQ/IN/NOT_IN: sorted value set
+    auto buf = std::make_unique<DevBuf>();
+    int rc;
+    if (is_float(c.type)) {
+      std::vector<double> v = p.vd;
+      if (v.empty())
+        for (int64_t x : p.vi) v.push_back((double)x);
+      if (c.type == T_FLOAT)
+        for (double& x : v) x = (double)(float)x;
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      L->kind = LEAF_RAW_IN_F;
+      L->in_n = (int32_t)v.size();
+      rc = buf->alloc_copy(v.data(), v.size() * 8, 64);
+      if (rc) return rc;
+      L->in_d = (const double*)buf->p;
+    } else {
+      std::vector<int64_t> v = p.vi;
+      if (v.empty())
+        for (double x : p.vd) v.push_back((int64_t)x);
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      L->kind = LEAF_RAW_IN_I;
+      L->in_n = (int32_t)v.size();
+      rc = buf->alloc_copy(v.data(), v.size() * 8, 64);
+      if (rc) return rc;
+      L->in_i = (const int64_t*)buf->p;
+    }
+    r->owned.push_back(std::move(buf));
+    return 0;
+  }
+
+  // dictionary-based evaluators: resolve to a dictId range or dictId set in this segment
+  int64_t start = 0, end = 0;
+  std::vector<int32_t> ids;
+  bool is_range = false;
+  if (p.type == PINOT_AMD_RANGE) {
+    dict_range_of(p, c, &start, &end);
+    if (end < start) end = start;
+    is_range = true;
+  } else {
+    ids = dict_ids_of_values(p, c);
+    if (!ids.empty() && ids.back() - ids.front() + 1 == (int32_t)ids.size()) {
+      is_range = true;
+      start = ids.front();
+      end = (int64_t)ids.back() + 1;
+    } else if (ids.empty()) {
+      is_range = true;
+      start = end = 0;
+    }
+  }
+  const bool empty = is_range ? end <= start : ids.empty();
+  const bool full = is_range ? (start <= 0 && end >= c.card) : (int64_t)ids.size() == c.card;
+  if (empty || full) {  // alwaysFalse / alwaysTrue evaluators
+    L->kind = LEAF_CONST;
+    L->lo_i = full ? 1 : 0;
+    *needs_slot = false;
+    L->slot = -1;
+    return 0;
+  }
+  if (c.enc == ENC_SORTED && is_range) {
+    // SortedIndexBasedFilterOperator: a dictId range of a sorted column is one docId range
+    L->kind = LEAF_DOC_RANGE;
+    L->lo_i = c.sorted_start[start];
+    L->hi_i = c.sorted_end[end - 1];
+    L->slot = -1;
+    *needs_slot = false;
+    return 0;
+  }
+  if (p.use_inv && c.has_inv) {
+    // BitmapBasedFilterOperator: OR of the inverted-index bitmaps of the matching dictIds
+    if (is_range) {
+      ids.clear();
+      for (int64_t d = start; d < end; ++d) ids.push_back((int32_t)d);
+    }
+    std::vector<int32_t> sel;
+    for (int32_t d : ids)
+      for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k) sel.push_back((int32_t)k);
+    const int64_t tiles = (seg->num_docs + kTileDocs - 1) / kTileDocs;
+    auto bs = std::make_unique<DevBuf>();
+    int rc = bs->alloc((size_t)std::max<int64_t>(tiles, 1) * kTileDocs / 8 + 64);
+    if (rc) return rc;
+    auto sb = std::make_unique<DevBuf>();
+    rc = sb->alloc_copy(sel.data(), sel.size() * 4, 64);
+    if (rc) return rc;
+    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), (int32_t)sel.size(), seg->num_docs});
+    L->kind = LEAF_DOC_BITSET;
+    L->bits = (const uint32_t*)bs->p;
+    L->slot = -1;
+    *needs_slot = false;
+    r->owned.push_back(std::move(bs));
+    r->owned.push_back(std::move(sb));
+    return 0;
+  }
+  if (is_range) {
+    L->kind = LEAF_DICT_RANGE;
+    L->lo_i = start;
+    L->hi_i = end;
+    return 0;
+  }
+  std::vector<uint32_t> mask(((size_t)c.card + 31) / 32 + 1, 0u);
+  for (int32_t d : ids) mask[d >> 5] |= 1u << (d & 31);
+  auto buf = std::make_unique<DevBuf>();
+  int rc = buf->alloc_copy(mask.data(), mask.size() * 4, 64);
+  if (rc) return rc;
+  L->kind = LEAF_DICT_SET;
+  L->bits = (const uint32_t*)buf->p;
+  r->owned.push_back(std::move(buf));
+  return 0;
+}
+
+static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
+                             MergedKeyColumn* out) {
+  const Column* c0 = segs[0]->cols.at(col).get();
+  out->type = c0->type;
+  for (auto* s : segs) {
+    const Column* c = s->cols.at(col).get();
+    if (c->type != c0->type) return fail(PINOT_AMD_EINVAL, "group-by column %s has different types", col.c_str());
+    if (c->type == T_STRING) out->vs.insert(out->vs.end(), c->dict_s.begin(), c->dict_s.end());
+    else if (is_float(c->type)) out->vd.insert(out->vd.end(), c->dict_d.begin(), c->dict_d.end());
+    else out->vi.insert(out->vi.end(), c->dict_i.begin(), c->dict_i.end());
+  }
+  if (out->type == T_STRING) {
+    std::sort(out->vs.begin(), out->vs.end(), java_less);
+    out->vs.erase(std::unique(out->vs.begin(), out->vs.end()), out->vs.end());
+  } else if (is_float(out->type)) {
+    std::sort(out->vd.begin(), out->vd.end());
+    out->vd.erase(std::unique(out->vd.begin(), out->vd.end()), out->vd.end());
+  } else {
+    std::sort(out->vi.begin(), out->vi.end());
+    out->vi.erase(std::unique(out->vi.begin(), out->vi.end()), out->vi.end());
+  }
+  return 0;
+}
+
+static int remap_for(const Column& c, const MergedKeyColumn& m, std::vector<int32_t>* out) {
+  out->resize(c.card);
+  for (int32_t d = 0; d < c.card; ++d) {
+    int64_t pos;
+    if (c.type == T_STRING)
+      pos = std::lower_bound(m.vs.begin(), m.vs.end(), c.dict_s[d], java_less) - m.vs.begin();
+    else if (is_float(c.type))
+      pos = std::lower_bound(m.vd.begin(), m.vd.end(), c.dict_d[d]) - m.vd.begin();
+    else
+      pos = std::lower_bound(m.vi.begin(), m.vi.end(), c.dict_i[d]) - m.vi.begin();
+    (*out)[d] = (int32_t)pos;
+  }
+  return 0;
+}
+
+static int run_plan(pinot_amd_result* r) {
+  hipStream_t st = r->stream;
+  // inverted-index leaves: expand roaring containers into dense doc bitsets
+  for (auto& il : r->inv_leaves) {
+    HIP_OK(hipMemsetAsync(il.bitset->p, 0, il.bitset->n, st));
+    HIP_OK(launch_roaring_expand((const uint8_t*)il.col->inv.p, il.col->inv_conts.p, (const int32_t*)il.sel->p,
+                                 il.nsel, il.num_docs, (uint64_t*)il.bitset->p, st));
+  }
+  HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
+  if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
+  HIP_OK(hipEventRecord(r->ev0, st));
+  HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p, nullptr,
+                     (unsigned long long*)r->matched.p, r->grid, st));
+  HIP_OK(hipEventRecord(r->ev1, st));
+  return 0;
+}
+
+extern "C" {
+
+int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
+                      pinot_amd_result** out) {
+  if (!qq || !segs_in || n < 1 || !out) return fail(PINOT_AMD_EINVAL, "execute: bad arguments");
+  std::vector<pinot_amd_segment*> segs(segs_in, segs_in + n);
+  auto res = std::make_unique<pinot_amd_result>();
+  pinot_amd_result* r = res.get();
+  r->stream = (hipStream_t)stream;
+  const pinot_amd_query& Q = *qq;
+
+  // ---- slots: columns the kernel must decode ----
+  std::vector<std::string> slot_cols;
+  auto slot_of = [&](const std::string& name) -> int {
+    for (size_t i = 0; i < slot_cols.size(); ++i)
+      if (slot_cols[i] == name) return (int)i;
+    slot_cols.push_back(name);
+    return (int)slot_cols.size() - 1;
+  };
+  for (auto* s : segs) {
+    auto need = [&](const std::string& col) -> int {
+      if (!s->cols.count(col)) return fail(PINOT_AMD_EINVAL, "segment %s has no column %s", s->name.c_str(), col.c_str());
+      return 0;
+    };
+    for (auto& p : Q.preds) if (int rc = need(p.column)) return rc;
+    for (auto& g : Q.group_by) if (int rc = need(g)) return rc;
+    for (auto& a : Q.aggs) if (!a.column.empty()) if (int rc = need(a.column)) return rc;
+  }
+  // group-by + aggregation columns always need decoding; predicate columns only if some segment's
+  // leaf reads values (decided below)
+  for (auto& g : Q.group_by) {
+    const Column& c = *segs[0]->cols.at(g);
+    if (c.enc == ENC_RAW) return fail(PINOT_AMD_EUNSUPPORTED, "GROUP BY on raw column %s", g.c_str());
+    slot_of(g);
+  }
+  for (auto& a : Q.aggs) {
+    if (a.column.empty()) continue;
+    const Column& c = *segs[0]->cols.at(a.column);
+    if (c.type == T_STRING) return fail(PINOT_AMD_EINVAL, "cannot aggregate STRING column %s", a.column.c_str());
+    slot_of(a.column);
+  }
+
+  // ---- per-segment leaves ----
+  const size_t np = Q.preds.size();
+  std::vector<std::vector<DevLeaf>> seg_leaves(n, std::vector<DevLeaf>(np));
+  std::vector<std::vector<int>> leaf_slot_col(n, std::vector<int>(np, -1));  // predicate -> slot (or -1)
+  int nclauses = 0;
+  for (size_t pi = 0; pi < np; ++pi) nclauses = std::max(nclauses, Q.preds[pi].clause + 1);
+  for (int si = 0; si < n; ++si) {
+    for (size_t pi = 0; pi < np; ++pi) {
+      const PredSpec& p = Q.preds[pi];
+      const Column& c = *segs[si]->cols.at(p.column);
+      bool needs_slot = false;
+      int rc = make_leaf_for_segment(r, si, segs[si], p, c, -1, &seg_leaves[si][pi], &needs_slot, r->stream);
+      if (rc) return rc;
+      if (needs_slot) leaf_slot_col[si][pi] = slot_of(p.column);
+    }
+  }
+  if ((int)slot_cols.size() > kMaxSlots) return fail(PINOT_AMD_EUNSUPPORTED, "query reads %zu columns (max %d)",
+                                                    slot_cols.size(), kMaxSlots);
+  const int nslots = (int)slot_cols.size();
+
+  // leaf order must be the same for all segments: group by the slot the leaf reads in the
+  // segment where it reads one; a predicate whose leaf is slot-less in some segments keeps its
+  // position and the slot-less segments get a LEAF_CONST/DOC leaf evaluated in that position.
+  // Simplest uniform layout: per predicate choose "slot position" = the slot if any segment needs
+  // it, else slot-less.
+  std::vector<int> pred_slot(np, -1);
+  for (size_t pi = 0; pi < np; ++pi)
+    for (int si = 0; si < n; ++si)
+      if (leaf_slot_col[si][pi] >= 0) pred_slot[pi] = leaf_slot_col[si][pi];
+  std::vector<size_t> order;  // predicates sorted by slot, slot-less last
+  for (int sl = 0; sl < nslots; ++sl)
+    for (size_t pi = 0; pi < np; ++pi)
+      if (pred_slot[pi] == sl) order.push_back(pi);
+  const int slotless_begin = (int)order.size();
+  for (size_t pi = 0; pi < np; ++pi)
+    if (pred_slot[pi] < 0) order.push_back(pi);
+
+  DevQuery& q = r->q;
+  memset(&q, 0, sizeof(q));
+  q.nsegs = n;
+  q.nslots = nslots;
+  q.nleaves = (int32_t)np;
+  q.nclauses = nclauses;
+  {
+    int pos = 0;
+    for (int sl = 0; sl < nslots; ++sl) {
+      q.slot_leaf_begin[sl] = pos;
+      for (size_t pi = 0; pi < np; ++pi)
+        if (pred_slot[pi] == sl) ++pos;
+    }
+    for (int sl = nslots; sl <= kMaxSlots; ++sl) q.slot_leaf_begin[sl] = pos;
+    q.slotless_leaf_begin = slotless_begin;
+    q.slotless_leaf_end = (int32_t)np;
+  }
+
+  // ---- group-by key space ----
+  r->num_group_by = (int32_t)Q.group_by.size();
+  int64_t num_keys = 1;
+  std::vector<std::vector<int32_t>> remaps;  // [g][seg] handled below
+  for (auto& g : Q.group_by) {
+    MergedKeyColumn m;
+    int rc = build_merged_keys(segs, g, &m);
+    if (rc) return rc;
+    r->key_stride.push_back(num_keys);
+    const double nk = (double)num_keys * (double)std::max<size_t>(m.size(), 1);
+    if (nk > (double)(1ll << 31)) return fail(PINOT_AMD_EUNSUPPORTED, "group key space %.0f exceeds the dense table", nk);
+    num_keys *= (int64_t)std::max<size_t>(m.size(), 1);
+    r->keys.push_back(std::move(m));
+  }
+  q.num_keys = num_keys;
+
+  // ---- accumulators: acc 0 = COUNT; others grouped by slot ----
+  struct AccReq { int slot; int op; };
+  std::vector<AccReq> reqs;
+  std::vector<int> agg_req(Q.aggs.size(), -1);
+  for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
+    const AggSpec& a = Q.aggs[ai];
+    if (a.type == PINOT_AMD_AGG_COUNT) continue;
+    const Column& c = *segs[0]->cols.at(a.column);
+    int op;
+    switch (a.type) {
+      case PINOT_AMD_AGG_SUM:
+      case PINOT_AMD_AGG_AVG:
+        op = is_float(c.type) ? ACC_SUM_F64 : ACC_SUM_I64;
+        break;
+      case PINOT_AMD_AGG_SUMLONG:
+        if (is_float(c.type)) return fail(PINOT_AMD_EINVAL, "SUMLONG on floating column %s", a.column.c_str());
+        op = ACC_SUM_I64;
+        break;
+      case PINOT_AMD_AGG_MIN: op = ACC_MIN; break;
+      default: op = ACC_MAX; break;
+    }
+    const int sl = slot_of(a.column);
+    int found = -1;
+    for (size_t k = 0; k < reqs.size(); ++k)
+      if (reqs[k].slot == sl && reqs[k].op == op) found = (int)k;
+    if (found < 0) {
+      reqs.push_back({sl, op});
+      found = (int)reqs.size() - 1;
+    }
+    agg_req[ai] = found;
+  }
+  if ((int)reqs.size() + 1 > kMaxAcc) return fail(PINOT_AMD_EUNSUPPORTED, "too many aggregations");
+  std::vector<int> req_acc(reqs.size());
+  q.nacc = 1;
+  q.acc_op[0] = ACC_COUNT;
+  for (int sl = 0; sl < kMaxSlots; ++sl) {
+    q.slot_acc_begin[sl] = q.nacc;
+    for (size_t k = 0; k < reqs.size(); ++k)
+      if (reqs[k].slot == sl) {
+        req_acc[k] = q.nacc;
+        q.acc_op[q.nacc++] = reqs[k].op;
+      }
+  }
+  q.slot_acc_begin[kMaxSlots] = q.nacc;
+  for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
+    r->agg_type.push_back(Q.aggs[ai].type);
+    r->agg_acc.push_back(agg_req[ai] < 0 ? 0 : req_acc[agg_req[ai]]);
+  }
+  for (size_t j = 0; j < Q.group_by.size(); ++j) q.slot_group_stride[slot_of(Q.group_by[j])] = r->key_stride[j];
+  if (Q.aggs.empty() && Q.group_by.empty()) q.nacc = 0;  // filter-only: count matches
+
+  // LDS-privatised table when it fits in 40 KB (keeps >= 4 blocks of 256 threads per CU)
+  const int64_t lds_bytes = (int64_t)q.nacc * num_keys * 8;
+  q.lds_keys = (q.nacc > 0 && lds_bytes <= 40 * 1024) ? (int32_t)num_keys : 0;
+
+  // ---- device segments ----
+  r->hsegs.resize(n);
+  int64_t tiles = 0;
+  for (int si = 0; si < n; ++si) {
+    DevSegment& ds = r->hsegs[si];
+    memset(&ds, 0, sizeof(ds));
+    ds.num_docs = segs[si]->num_docs;
+    ds.tile_begin = tiles;
+    tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
+    for (int sl = 0; sl < nslots; ++sl) {
+      const Column& c = *segs[si]->cols.at(slot_cols[sl]);
+      DevColumn& dc = ds.cols[sl];
+      dc.data = (const uint8_t*)c.fwd.p;
+      dc.dict = c.dict.p;
+      dc.enc = c.enc;
+      dc.type = c.type;
+      dc.bits = c.bits;
+      dc.card = c.card;
+    }
+    for (size_t j = 0; j < Q.group_by.size(); ++j) {
+      const Column& c = *segs[si]->cols.at(Q.group_by[j]);
+      std::vector<int32_t> rm;
+      remap_for(c, r->keys[j], &rm);
+      bool identity = (int64_t)rm.size() == (int64_t)r->keys[j].size();
+      for (size_t d = 0; identity && d < rm.size(); ++d) identity = rm[d] == (int32_t)d;
+      if (!identity) {
+        auto buf = std::make_unique<DevBuf>();
+        int rc = buf->alloc_copy(rm.data(), rm.size() * 4, 64);
+        if (rc) return rc;
+        ds.cols[slot_of(Q.group_by[j])].remap = (const int32_t*)buf->p;
+        r->owned.push_back(std::move(buf));
+      }
+    }
+    for (size_t k = 0; k < order.size(); ++k) {
+      DevLeaf L = seg_leaves[si][order[k]];
+      // leaves that resolved slot-less in this segment but sit in a slot group keep kind
+      // (CONST/DOC_*), which ignore the values
+      L.slot = pred_slot[order[k]];
+      ds.leaves[k] = L;
+    }
+  }
+  q.total_tiles = tiles;
+  if (tiles == 0) q.total_tiles = 0;
+
+  int rc = r->d_segs.alloc_copy(r->hsegs.data(), r->hsegs.size() * sizeof(DevSegment), 0);
+  if (rc) return rc;
+  rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * num_keys * 8);
+  if (rc) return rc;
+  rc = r->matched.alloc(8);
+  if (rc) return rc;
+
+  // persistent grid: enough blocks to fill every CU at the occupancy the LDS table allows
+  int dev = 0, cus = 256;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int per_cu = q.lds_keys > 0 ? std::max(1, std::min(8, (int)((160 * 1024) / std::max<int64_t>(lds_bytes, 1)))) : 8;
+  int64_t grid = (int64_t)cus * per_cu;
+  if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
+  r->grid = (int)grid;
+  HIP_OK(hipEventCreate(&r->ev0));
+  HIP_OK(hipEventCreate(&r->ev1));
+  rc = run_plan(r);
+  if (rc) return rc;
+  *out = res.release();
+  return 0;
+}
+
+int pinot_amd_execute_again(pinot_amd_result* r, void* stream) {
+  if (!r) return fail(PINOT_AMD_EINVAL, "execute_again: null result");
+  r->stream = (hipStream_t)stream;
+  return run_plan(r);
+}
+
+int pinot_amd_result_destroy(pinot_amd_result* r) {
+  delete r;
+  return 0;
+}
+
+int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
+  if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_docs_matched: bad arguments");
+  HIP_OK(hipMemcpyAsync(h_out, r->matched.p, 8, hipMemcpyDeviceToHost, r->stream));
+  HIP_OK(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
+int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms) {
+  if (!r || !h_ms) return fail(PINOT_AMD_EINVAL, "last_kernel_ms: bad arguments");
+  HIP_OK(hipEventSynchronize(r->ev1));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, r->ev0, r->ev1));
+  *h_ms = ms;
+  return 0;
+}
+
+static int fetch_acc(pinot_amd_result* r, std::vector<uint64_t>* h) {
+  const int64_t nk = r->q.num_keys;
+  h->resize((size_t)std::max(r->q.nacc, 1) * nk);
+  if (r->q.nacc == 0) return 0;
+  HIP_OK(hipMemcpyAsync(h->data(), r->acc.p, h->size() * 8, hipMemcpyDeviceToHost, r->stream));
+  HIP_OK(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
+int pinot_amd_result_num_groups(pinot_amd_result* r, int64_t* h_out) {
+  if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_groups: bad arguments");
+  if (r->num_group_by == 0) {
+    *h_out = 1;
+    return 0;
+  }
+  std::vector<uint64_t> h;
+  int rc = fetch_acc(r, &h);
+  if (rc) return rc;
+  int64_t g = 0;
+  for (int64_t k = 0; k < r->q.num_keys; ++k) g += h[k] != 0;
+  *h_out = g;
+  return 0;
+}
+
+static double decode_ordered(uint64_t u, int op) {
+  if (op == ACC_MIN && u == ~0ull) return INFINITY;
+  if (op == ACC_MAX && u == 0ull) return -INFINITY;
+  const uint64_t b = (u >> 63) ? (u & 0x7FFFFFFFFFFFFFFFull) : ~u;
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}
+
+int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, double* h_values, int64_t* h_values_i64,
+                           int64_t* h_num_fetched) {
+  if (!r || cap < 0 || !h_num_fetched) return fail(PINOT_AMD_EINVAL, "fetch: bad arguments");
+  std::vector<uint64_t> h;
+  int rc = fetch_acc(r, &h);
+  if (rc) return rc;
+  const int64_t nk = r->q.num_keys;
+  const int na = (int)r->agg_type.size();
+  int64_t g = 0;
+  for (int64_t k = 0; k < nk; ++k) {
+    const uint64_t cnt = r->q.nacc ? h[k] : 0;
+    if (r->num_group_by > 0 && cnt == 0) continue;
+    if (g >= cap) return fail(PINOT_AMD_EOVERFLOW, "fetch: more than %lld groups", (long long)cap);
+    if (h_keys) {
+      int64_t rem = k;
+      for (int j = 0; j < r->num_group_by; ++j) {
+        const MergedKeyColumn& m = r->keys[j];
+        const int64_t sz = (int64_t)std::max<size_t>(m.size(), 1);
+        const int64_t id = rem % sz;
+        rem /= sz;
+        int64_t out;
+        if (m.type == T_STRING) out = id;
+        else if (is_float(m.type)) memcpy(&out, &m.vd[id], 8);
+        else out = m.vi[id];
+        h_keys[g * r->num_group_by + j] = out;
+      }
+    }
+    for (int a = 0; a < na; ++a) {
+      const int acc = r->agg_acc[a];
+      const int op = r->q.acc_op[acc];
+      const uint64_t w = h[(size_t)acc * nk + k];
+      double v;
+      int64_t vi = 0;
+      switch (r->agg_type[a]) {
+        case PINOT_AMD_AGG_COUNT:
+          vi = (int64_t)cnt;
+          v = (double)vi;
+          break;
+        case PINOT_AMD_AGG_AVG: {
+          const double s = op == ACC_SUM_F64 ? ([&] { double d; memcpy(&d, &w, 8); return d; })() : (double)(int64_t)w;
+          v = cnt ? s / (double)cnt : -INFINITY;  // AvgAggregationFunction: empty -> DEFAULT_FINAL_RESULT
+          break;
+        }
+        case PINOT_AMD_AGG_MIN:
+        case PINOT_AMD_AGG_MAX:
+          v = decode_ordered(w, op);
+          break;
+        default:
+          if (op == ACC_SUM_F64) {
+            memcpy(&v, &w, 8);
+          } else {
+            vi = (int64_t)w;
+            v = (double)vi;
+          }
+      }
+      if (h_values) h_values[g * na + a] = v;
+      if (h_values_i64) h_values_i64[g * na + a] = vi;
+    }
+    ++g;
+  }
+  *h_num_fetched = g;
+  return 0;
+}
+
+const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t id) {
+  if (!r || j < 0 || j >= r->num_group_by) return nullptr;
+  const MergedKeyColumn& m = r->keys[j];
+  if (m.type != T_STRING || id < 0 || id >= (int64_t)m.vs.size()) return nullptr;
+  return m.vs[id].c_str();
+}
+
+int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
+                                  void** h_slot_ptrs, int32_t* h_slot_ops) {
+  if (!r || !h_num_slots || !h_num_key_slots) return fail(PINOT_AMD_EINVAL, "accumulators: bad arguments");
+  *h_num_slots = r->q.nacc;
+  *h_num_key_slots = r->q.num_keys;
+  for (int a = 0; a < r->q.nacc; ++a) {
+    if (h_slot_ptrs) h_slot_ptrs[a] = (uint8_t*)r->acc.p + (size_t)a * r->q.num_keys * 8;
+    if (h_slot_ops) {
+      const int op = r->q.acc_op[a];
+      h_slot_ops[a] = (op == ACC_COUNT || op == ACC_SUM_I64) ? 0 : op == ACC_SUM_F64 ? 1 : op == ACC_MIN ? 2 : 3;
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

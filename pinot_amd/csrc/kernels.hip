@@ -1,0 +1,725 @@
+// kernels.hip — gfx950 kernels for Pinot's segment scan / filter / aggregation / group-by.
+//
+// Layout in HBM: every column keeps the bytes Pinot writes for it — the fixed-bit
+// forward index as the big-endian MSB-first bit stream, raw values big-endian — so nothing is
+// transcoded at staging time; the kernels byte-swap in registers (v_perm_b32).
+//
+// Work decomposition: a block of 256 threads (4 wave64) owns a contiguous range of 1024-doc tiles
+// across the whole segment batch; each lane owns 4 consecutive docs of a tile, so a raw INT column
+// is one 16 B load per lane (1 KiB per wave instruction, fully coalesced) and a LONG/DOUBLE column
+// two. Filter, group-key and aggregation are fused in one pass; group accumulators live in LDS
+// when the key space fits and are merged into HBM with atomics once per block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_types.h"
+
+namespace pamd {
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint64_t bswap64(uint32_t hi_word_be, uint32_t lo_word_be) {
+  // bytes as stored: hi_word_be holds the first 4 bytes (most significant in BE order)
+  return ((uint64_t)bswap32(hi_word_be) << 32) | bswap32(lo_word_be);
+}
+__device__ __forceinline__ uint64_t ordered_from_double(double d) {
+  uint64_t u = (uint64_t)__double_as_longlong(d);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double u64_as_double(uint64_t u) { return __longlong_as_double((long long)u); }
+
+__device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return i == 0 ? a : i == 1 ? b : i == 2 ? c : d;
+}
+
+// 4 consecutive values of a big-endian MSB-first bit stream starting at doc0 (FixedBitIntReader /
+// PinotDataBitSet.readInt semantics). A 5-dword window always covers 4 values of <= 31 bits.
+__device__ __forceinline__ void load_fixed_bit4(const uint8_t* data, int bits, int64_t doc0, int64_t out[4]) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(data);
+  const int64_t bit0 = doc0 * bits;
+  const int64_t w0 = bit0 >> 5;
+  const uint32_t r = (uint32_t)(bit0 & 31);
+  const uint32_t x0 = bswap32(w[w0]), x1 = bswap32(w[w0 + 1]), x2 = bswap32(w[w0 + 2]),
+                 x3 = bswap32(w[w0 + 3]), x4 = bswap32(w[w0 + 4]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t p = r + (uint32_t)(k * bits);
+    const uint32_t i = p >> 5, sh = p & 31;
+    const uint64_t win = ((uint64_t)sel4(i, x0, x1, x2, x3) << 32) | sel4(i, x1, x2, x3, x4);
+    out[k] = (int64_t)((win << sh) >> (64 - bits));
+  }
+}
+
+// dictId of a doc of a sorted column: last dictId whose first doc <= doc (SortedIndexReaderImpl).
+__device__ __forceinline__ int32_t sorted_dict_id(const int32_t* starts, int32_t card, int64_t doc) {
+  int32_t lo = 0, hi = card - 1;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if ((int64_t)starts[mid] <= doc) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Decoded per-slot representation: dictIds (dict columns), INT/LONG values, or FLOAT/DOUBLE as
+// double bits.
+__device__ __forceinline__ void load_slot(const DevColumn& c, int64_t doc0, int64_t v[4]) {
+  if (c.enc == ENC_FIXED_BIT) {
+    load_fixed_bit4(c.data, c.bits, doc0, v);
+  } else if (c.enc == ENC_RAW) {
+    if (c.type == T_INT || c.type == T_FLOAT) {
+      const uint4 q = *reinterpret_cast<const uint4*>(c.data + doc0 * 4);
+      const uint32_t e[4] = {bswap32(q.x), bswap32(q.y), bswap32(q.z), bswap32(q.w)};
+      if (c.type == T_INT) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (int64_t)(int32_t)e[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __double_as_longlong((double)__uint_as_float(e[k]));
+      }
+    } else {
+      const uint4 a = *reinterpret_cast<const uint4*>(c.data + doc0 * 8);
+      const uint4 b = *reinterpret_cast<const uint4*>(c.data + doc0 * 8 + 16);
+      v[0] = (int64_t)bswap64(a.x, a.y);
+      v[1] = (int64_t)bswap64(a.z, a.w);
+      v[2] = (int64_t)bswap64(b.x, b.y);
+      v[3] = (int64_t)bswap64(b.z, b.w);
+    }
+  } else {  // ENC_SORTED
+    const int32_t* starts = reinterpret_cast<const int32_t*>(c.data);
+    int32_t id = sorted_dict_id(starts, c.card, doc0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      while (id + 1 < c.card && (int64_t)starts[id + 1] <= doc0 + k) ++id;
+      v[k] = id;
+    }
+  }
+}
+
+// value of slot element as int64 (for SUM on integer columns) — dict columns go through the
+// dictionary (BlockValSet.getLongValuesSV over Dictionary.readLongValues)
+__device__ __forceinline__ int64_t slot_value_i64(const DevColumn& c, int64_t x) {
+  if (c.enc == ENC_RAW) return x;
+  return c.type == T_INT ? (int64_t) reinterpret_cast<const int32_t*>(c.dict)[x]
+                         : reinterpret_cast<const int64_t*>(c.dict)[x];
+}
+// value as double (SUM on FLOAT/DOUBLE, MIN, MAX: Pinot aggregates these in double)
+__device__ __forceinline__ double slot_value_f64(const DevColumn& c, int64_t x) {
+  if (c.enc == ENC_RAW) {
+    return (c.type == T_INT || c.type == T_LONG) ? (double)x : __longlong_as_double(x);
+  }
+  switch (c.type) {
+    case T_INT: return (double)reinterpret_cast<const int32_t*>(c.dict)[x];
+    case T_LONG: return (double)reinterpret_cast<const int64_t*>(c.dict)[x];
+    case T_FLOAT: return (double)reinterpret_cast<const float*>(c.dict)[x];
+    default: return reinterpret_cast<const double*>(c.dict)[x];
+  }
+}
+
+__device__ __forceinline__ bool in_sorted_i64(const int64_t* a, int32_t n, int64_t v) {
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && a[lo] == v;
+}
+__device__ __forceinline__ bool in_sorted_f64(const double* a, int32_t n, double v) {
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && a[lo] == v;
+}
+
+// one predicate leaf over the lane's 4 docs -> 4-bit mask
+__device__ __forceinline__ uint32_t eval_leaf(const DevLeaf& L, const int64_t v[4], int64_t doc0) {
+  uint32_t m = 0;
+  switch (L.kind) {
+    case LEAF_DICT_RANGE:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= (uint32_t)(v[k] >= L.lo_i && v[k] < L.hi_i) << k;
+      break;
+    case LEAF_DICT_SET:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= ((L.bits[v[k] >> 5] >> (v[k] & 31)) & 1u) << k;
+      break;
+    case LEAF_RAW_RANGE_I:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= (uint32_t)(v[k] >= L.lo_i && v[k] <= L.hi_i) << k;
+      break;
+    case LEAF_RAW_RANGE_F:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double d = __longlong_as_double(v[k]);
+        m |= (uint32_t)(d >= L.lo_d && d <= L.hi_d) << k;
+      }
+      break;
+    case LEAF_RAW_IN_I:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= (uint32_t)in_sorted_i64(L.in_i, L.in_n, v[k]) << k;
+      break;
+    case LEAF_RAW_IN_F:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= (uint32_t)in_sorted_f64(L.in_d, L.in_n, __longlong_as_double(v[k])) << k;
+      break;
+    case LEAF_DOC_RANGE:
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m |= (uint32_t)(doc0 + k >= L.lo_i && doc0 + k <= L.hi_i) << k;
+      break;
+    case LEAF_DOC_BITSET: {
+      // doc0 is a multiple of 4: the 4 bits sit in one 32-bit word
+      m = (L.bits[doc0 >> 5] >> (doc0 & 31)) & 0xFu;
+      break;
+    }
+    default:  // LEAF_CONST
+      m = L.lo_i ? 0xFu : 0u;
+      break;
+  }
+  return L.negate ? (~m & 0xFu) : m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// wave reductions (64 lanes)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ double wave_sum_f64(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(x, o, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+// accumulator update at a table word (LDS or HBM; generic address space resolves both)
+__device__ __forceinline__ void acc_apply(int32_t op, uint64_t* p, uint64_t bits) {
+  switch (op) {
+    case ACC_COUNT:
+    case ACC_SUM_I64:
+      atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+      break;
+    case ACC_SUM_F64:
+      unsafeAtomicAdd(reinterpret_cast<double*>(p), u64_as_double(bits));
+      break;
+    case ACC_MIN:
+      atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+      break;
+    default:
+      atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+      break;
+  }
+}
+
+__device__ __forceinline__ uint64_t acc_identity(int32_t op) {
+  if (op == ACC_MIN) return ~0ull;
+  return 0ull;  // COUNT/SUM: 0 (also +0.0 for f64); MAX: ordered 0 is below every double
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused filter + group-by + aggregation over a batch of segments.
+//   kBitset: also write the filter's docId bitset (per segment, at bitset_out[s] words)
+//   kLds:    accumulate into an LDS-privatised table of q.lds_keys keys, flushed once per block
+// ------------------------------------------------------------------------------------------------
+template <bool kLds, bool kBitset>
+__global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restrict__ segs, const DevQuery q,
+                                                      uint64_t* __restrict__ acc,      // [nacc][num_keys]
+                                                      uint64_t* const* __restrict__ bitset_out,
+                                                      unsigned long long* __restrict__ matched_out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds_table[];  // [nacc][lds_keys]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+
+  if constexpr (kLds) {
+    const int n = q.nacc * q.lds_keys;
+    for (int i = tid; i < n; i += kBlock) lds_table[i] = acc_identity(q.acc_op[i / q.lds_keys]);
+    __syncthreads();
+  }
+  uint64_t* const table = kLds ? lds_table : acc;
+  const int64_t tstride = kLds ? (int64_t)q.lds_keys : q.num_keys;
+
+  // contiguous tile range of this block
+  const int64_t per = (q.total_tiles + gridDim.x - 1) / gridDim.x;
+  const int64_t t_begin = (int64_t)blockIdx.x * per;
+  const int64_t t_end = min(q.total_tiles, t_begin + per);
+  int64_t matched = 0;
+
+  int s = 0;
+  if (t_begin < t_end) {
+    // last segment whose tile_begin <= t_begin (wave-uniform binary search)
+    int lo = 0, hi = q.nsegs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].tile_begin <= t_begin) lo = mid; else hi = mid - 1;
+    }
+    s = lo;
+  }
+
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    while (s + 1 < q.nsegs && segs[s + 1].tile_begin <= t) ++s;
+    const DevSegment& seg = segs[s];
+    const int64_t doc0 = (t - seg.tile_begin) * kTileDocs + (int64_t)tid * kDocsPerThread;
+    const int64_t nd = seg.num_docs;
+    uint32_t match = doc0 + 4 <= nd ? 0xFu : doc0 >= nd ? 0u : (0xFu >> (4 - (nd - doc0)));
+
+    // ---- decode every referenced column (compile-time slot indices only) ----
+    int64_t v[kMaxSlots][4];
+#pragma unroll
+    for (int sl = 0; sl < kMaxSlots; ++sl) {
+      if (sl < q.nslots) load_slot(seg.cols[sl], doc0, v[sl]);
+    }
+
+    // ---- filter: AND over clauses of OR over leaves ----
+    if (q.nleaves > 0) {
+      uint64_t clause_bits = 0;
+#pragma unroll
+      for (int sl = 0; sl < kMaxSlots; ++sl) {
+        if (sl < q.nslots) {
+          for (int l = q.slot_leaf_begin[sl]; l < q.slot_leaf_begin[sl + 1]; ++l) {
+            const DevLeaf& L = seg.leaves[l];
+            clause_bits |= (uint64_t)eval_leaf(L, v[sl], doc0) << (4 * L.clause);
+          }
+        }
+      }
+      for (int l = q.slotless_leaf_begin; l < q.slotless_leaf_end; ++l) {
+        const DevLeaf& L = seg.leaves[l];
+        clause_bits |= (uint64_t)eval_leaf(L, v[0], doc0) << (4 * L.clause);
+      }
+      for (int c = 0; c < q.nclauses; ++c) match &= (uint32_t)(clause_bits >> (4 * c)) & 0xFu;
+    }
+
+    if constexpr (kBitset) {
+      // lane l holds bits for docs doc0..doc0+3 = bits 4*(l%16).. of word (tile*16 + tid/16)
+      uint64_t w = (uint64_t)match << (4 * (lane & 15));
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) w |= __shfl_xor(w, o, 64);
+      if ((lane & 15) == 0) bitset_out[s][(doc0 >> 6)] = w;
+    }
+
+    matched += __builtin_popcount(match);
+    if (q.nacc == 0) continue;
+
+    // ---- group key per doc ----
+    int64_t key[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int sl = 0; sl < kMaxSlots; ++sl) {
+      if (sl < q.nslots && q.slot_group_stride[sl] > 0) {
+        const int32_t* remap = seg.cols[sl].remap;
+        const int64_t st = q.slot_group_stride[sl];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) key[k] += (int64_t)(remap ? remap[v[sl][k]] : (int32_t)v[sl][k]) * st;
+      }
+    }
+
+    // ---- aggregation ----
+    // wave-uniform key fast path: every matching doc of the wave falls in one group (always true
+    // for aggregation-only queries; common for sorted time columns)
+    const bool lane_has = match != 0;
+    const int first_k = lane_has ? __builtin_ctz(match) : 0;
+    const int64_t kA = key[first_k];
+    bool lane_uniform = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lane_uniform &= !((match >> k) & 1) || key[k] == kA;
+    const unsigned long long has_mask = __ballot(lane_has);
+    if (has_mask == 0) continue;
+    const int src = __ffsll((long long)has_mask) - 1;
+    const int64_t kW = __shfl(kA, src, 64);
+    const bool wave_uniform = __ballot(lane_has && (!lane_uniform || kA != kW)) == 0;
+
+    if (wave_uniform) {
+      uint64_t* row = table + kW;
+      const int64_t cnt = wave_sum_i64(__builtin_popcount(match));
+      if (lane == 0) acc_apply(ACC_COUNT, row, (uint64_t)cnt);
+#pragma unroll
+      for (int sl = 0; sl < kMaxSlots; ++sl) {
+        if (sl < q.nslots) {
+          const DevColumn& col = seg.cols[sl];
+          for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
+            const int32_t op = q.acc_op[a];
+            uint64_t r;
+            if (op == ACC_SUM_I64) {
+              int64_t p = 0;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) p += ((match >> k) & 1) ? slot_value_i64(col, v[sl][k]) : 0;
+              r = (uint64_t)wave_sum_i64(p);
+            } else if (op == ACC_SUM_F64) {
+              double p = 0.0;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) p += ((match >> k) & 1) ? slot_value_f64(col, v[sl][k]) : 0.0;
+              r = (uint64_t)__double_as_longlong(wave_sum_f64(p));
+            } else if (op == ACC_MIN) {
+              uint64_t p = ~0ull;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const double d = slot_value_f64(col, v[sl][k]);
+                const uint64_t o = ordered_from_double(d);
+                if (((match >> k) & 1) && d == d && o < p) p = o;
+              }
+              r = wave_min_u64(p);
+            } else {
+              uint64_t p = 0;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const double d = slot_value_f64(col, v[sl][k]);
+                const uint64_t o = ordered_from_double(d);
+                if (((match >> k) & 1) && d == d && o > p) p = o;
+              }
+              r = wave_max_u64(p);
+            }
+            if (lane == 0) acc_apply(op, row + (int64_t)a * tstride, r);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((match >> k) & 1) {
+          uint64_t* row = table + key[k];
+          acc_apply(ACC_COUNT, row, 1);
+#pragma unroll
+          for (int sl = 0; sl < kMaxSlots; ++sl) {
+            if (sl < q.nslots) {
+              const DevColumn& col = seg.cols[sl];
+              for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
+                const int32_t op = q.acc_op[a];
+                uint64_t r;
+                if (op == ACC_SUM_I64) {
+                  r = (uint64_t)slot_value_i64(col, v[sl][k]);
+                } else {
+                  const double d = slot_value_f64(col, v[sl][k]);
+                  if (op != ACC_SUM_F64 && d != d) continue;  // MIN/MAX skip NaN (`value < min`)
+                  r = op == ACC_SUM_F64 ? (uint64_t)__double_as_longlong(d) : ordered_from_double(d);
+                }
+                acc_apply(op, row + (int64_t)a * tstride, r);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---- per-block results ----
+  {
+    const int64_t wm = wave_sum_i64(matched);
+    if (lane == 0 && wm) atomicAdd(matched_out, (unsigned long long)wm);
+  }
+  if constexpr (kLds) {
+    __syncthreads();
+    for (int g = tid; g < q.lds_keys; g += kBlock) {
+      if (lds_table[g] == 0) continue;  // no matching doc in this block for key g
+      for (int a = 0; a < q.nacc; ++a)
+        acc_apply(q.acc_op[a], acc + (int64_t)a * q.num_keys + g, lds_table[(int64_t)a * q.lds_keys + g]);
+    }
+  }
+}
+
+__global__ void init_acc_kernel(uint64_t* acc, int64_t num_keys, DevQuery q) {
+  const int64_t n = (int64_t)q.nacc * num_keys;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc[i] = acc_identity(q.acc_op[i / num_keys]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Low-level operators
+// ------------------------------------------------------------------------------------------------
+
+// FixedBitSVForwardIndexReaderV2.readDictIds over [start, start+len): 4 docs per lane
+__global__ void read_dict_ids_kernel(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out) {
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 >= len) return;
+  int64_t v[4];
+  const int64_t doc0 = start + i0;
+  // doc0 need not be 4-aligned here; the 5-dword window covers any start
+  load_fixed_bit4(packed, bits, doc0, v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (i0 + k < len) out[i0 + k] = (int32_t)v[k];
+}
+
+// FixedBitSVForwardIndexWriter: each lane packs 8 values = exactly `bits` bytes, no overlap
+__global__ void pack_dict_ids_kernel(const int32_t* values, int64_t n, int bits, uint8_t* packed) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 8 values
+  const int64_t v0 = g * 8;
+  if (v0 >= n) return;
+  unsigned __int128 acc = 0;  // up to 8 * 31 = 248 bits
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t x = v0 + k < n ? (uint32_t)values[v0 + k] : 0u;
+    acc = (acc << bits) | (unsigned __int128)(x & ((bits == 32) ? 0xFFFFFFFFu : ((1u << bits) - 1)));
+  }
+  // acc holds 8*bits bits, MSB first
+  const int nbytes = bits;  // 8 values * bits / 8
+  const int64_t byte0 = g * bits;
+  const int64_t total_bytes = (n * bits + 7) / 8;
+  for (int b = 0; b < nbytes; ++b) {
+    if (byte0 + b < total_bytes) packed[byte0 + b] = (uint8_t)(acc >> (8 * (nbytes - 1 - b)));
+  }
+}
+
+// raw BE values -> native LE values
+__global__ void read_raw_kernel(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  if (type == T_INT || type == T_FLOAT) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(raw + (start + i) * 4);
+    reinterpret_cast<uint32_t*>(out)[i] = bswap32(x);
+  } else {
+    const uint2 x = *reinterpret_cast<const uint2*>(raw + (start + i) * 8);
+    reinterpret_cast<uint64_t*>(out)[i] = bswap64(x.x, x.y);
+  }
+}
+
+__global__ void bitset_binop_kernel(const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n, int op) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = op == 0 ? (a[i] & b[i]) : (a[i] | b[i]);
+}
+
+__global__ void bitset_not_kernel(const uint64_t* a, uint64_t* out, int64_t num_docs) {
+  const int64_t nw = (num_docs + 63) / 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t w = ~a[i];
+    if (i == nw - 1 && (num_docs & 63)) w &= (1ull << (num_docs & 63)) - 1;
+    out[i] = w;
+  }
+}
+
+// Compaction, pass 1: popcount per 1024-word chunk (65536 docs)
+constexpr int kCompactWords = 1024;
+__global__ void bitset_chunk_count_kernel(const uint64_t* bits, int64_t nwords, int64_t* chunk_counts) {
+  __shared__ int64_t wsum[kBlock / 64];
+  const int64_t base = (int64_t)blockIdx.x * kCompactWords;
+  int64_t c = 0;
+  for (int i = threadIdx.x; i < kCompactWords; i += kBlock) {
+    const int64_t w = base + i;
+    if (w < nwords) c += __popcll(bits[w]);
+  }
+  c = wave_sum_i64(c);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int i = 0; i < kBlock / 64; ++i) t += wsum[i];
+    chunk_counts[blockIdx.x] = t;
+  }
+}
+
+// pass 2: exclusive scan of chunk counts (single block, sequential over groups of 256)
+__global__ void exclusive_scan_kernel(int64_t* counts, int64_t n, int64_t* total) {
+  __shared__ int64_t buf[kBlock];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += kBlock) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t x = i < n ? counts[i] : 0;
+    buf[threadIdx.x] = x;
+    __syncthreads();
+    for (int o = 1; o < kBlock; o <<= 1) {
+      const int64_t y = threadIdx.x >= o ? buf[threadIdx.x - o] : 0;
+      __syncthreads();
+      buf[threadIdx.x] += y;
+      __syncthreads();
+    }
+    if (i < n) counts[i] = carry + buf[threadIdx.x] - x;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry += buf[kBlock - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// pass 3: each wave compacts 64 words (4096 docs) per step with ballot + mbcnt style prefix sums
+__global__ void bitset_compact_kernel(const uint64_t* bits, int64_t nwords, const int64_t* chunk_offsets,
+                                      int32_t* out) {
+  __shared__ int64_t wtot[kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kCompactWords;
+  int64_t off = chunk_offsets[blockIdx.x];
+  // the block walks its chunk in steps of 256 words (one word per lane)
+  for (int step = 0; step < kCompactWords; step += kBlock) {
+    const int64_t w = base + step + threadIdx.x;
+    const uint64_t word = w < nwords ? bits[w] : 0ull;
+    const int cnt = __popcll(word);
+    // inclusive scan of cnt across the wave
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int64_t wave_off = 0;
+    for (int i = 0; i < wave; ++i) wave_off += wtot[i];
+    int64_t pos = off + wave_off + incl - cnt;
+    uint64_t x = word;
+    while (x) {
+      const int b = __builtin_ctzll(x);
+      out[pos++] = (int32_t)(w * 64 + b);
+      x &= x - 1;
+    }
+    int64_t step_total = 0;
+    for (int i = 0; i < kBlock / 64; ++i) step_total += wtot[i];
+    off += step_total;
+    __syncthreads();
+  }
+}
+
+// Inverted index expansion: one block per (dictId, container) entry of a container directory
+// built at staging time. Sets the container's docs in the dense bitset (atomicOr: containers of
+// different dictIds share 64-bit words).
+struct RoaringContainer {
+  uint32_t key;      // high 16 bits of the docIds
+  uint32_t kind;     // 0 array, 1 bitmap, 2 run
+  uint32_t count;    // array: cardinality, run: number of runs
+  uint32_t pad;
+  uint64_t offset;   // byte offset of the container payload inside the staged inverted index
+};
+
+__global__ void roaring_expand_kernel(const uint8_t* inv, const RoaringContainer* conts, const int32_t* sel,
+                                      int64_t num_docs, unsigned long long* bitset) {
+  const RoaringContainer c = conts[sel[blockIdx.x]];
+  const uint8_t* p = inv + c.offset;
+  const int64_t base = (int64_t)c.key << 16;
+  if (c.kind == 1) {
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+      const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
+      const int64_t d = base + 64 * i;
+      if (w && d < num_docs) atomicOr(&bitset[d >> 6], (unsigned long long)w);
+    }
+  } else if (c.kind == 0) {
+    for (uint32_t i = threadIdx.x; i < c.count; i += blockDim.x) {
+      const int64_t d = base + (p[2 * i] | (p[2 * i + 1] << 8));
+      if (d < num_docs) atomicOr(&bitset[d >> 6], 1ull << (d & 63));
+    }
+  } else {
+    for (uint32_t r = 0; r < c.count; ++r) {
+      const uint8_t* q = p + 2 + 4 * r;
+      const int64_t s = base + (q[0] | (q[1] << 8));
+      const int64_t l = q[2] | (q[3] << 8);
+      for (int64_t d = s + threadIdx.x; d <= s + l; d += blockDim.x)
+        if (d < num_docs) atomicOr(&bitset[d >> 6], 1ull << (d & 63));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers (called from host.cpp)
+// ------------------------------------------------------------------------------------------------
+static inline unsigned grid_for(int64_t n, int per_block) {
+  int64_t g = (n + per_block - 1) / per_block;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
+                       unsigned long long* d_matched, int grid, hipStream_t st) {
+  const bool lds = q.lds_keys > 0;
+  const size_t shmem = lds ? (size_t)q.nacc * q.lds_keys * 8 : 0;
+  if (d_bitsets) {
+    if (lds)
+      hipLaunchKernelGGL((scan_kernel<true, true>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, d_bitsets,
+                         d_matched);
+    else
+      hipLaunchKernelGGL((scan_kernel<false, true>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
+                         d_bitsets, d_matched);
+  } else {
+    if (lds)
+      hipLaunchKernelGGL((scan_kernel<true, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, nullptr,
+                         d_matched);
+    else
+      hipLaunchKernelGGL((scan_kernel<false, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
+                         nullptr, d_matched);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st) {
+  const int64_t n = (int64_t)q.nacc * q.num_keys;
+  unsigned g = grid_for(n, kBlock);
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(init_acc_kernel, dim3(g), dim3(kBlock), 0, st, d_acc, q.num_keys, q);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(read_dict_ids_kernel, dim3(grid_for((len + 3) / 4, kBlock)), dim3(kBlock), 0, st, packed, bits,
+                     start, len, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st) {
+  hipLaunchKernelGGL(pack_dict_ids_kernel, dim3(grid_for((n + 7) / 8, kBlock)), dim3(kBlock), 0, st, values, n, bits,
+                     packed);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_raw(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(read_raw_kernel, dim3(grid_for(len, kBlock)), dim3(kBlock), 0, st, raw, type, start, len, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_bitset_binop(const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n, int op,
+                               hipStream_t st) {
+  unsigned g = grid_for(n, kBlock);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(bitset_binop_kernel, dim3(g), dim3(kBlock), 0, st, a, b, out, n, op);
+  return hipGetLastError();
+}
+
+hipError_t launch_bitset_not(const uint64_t* a, uint64_t* out, int64_t num_docs, hipStream_t st) {
+  unsigned g = grid_for((num_docs + 63) / 64, kBlock);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(bitset_not_kernel, dim3(g), dim3(kBlock), 0, st, a, out, num_docs);
+  return hipGetLastError();
+}
+
+int64_t compact_num_chunks(int64_t num_docs) { return ((num_docs + 63) / 64 + kCompactWords - 1) / kCompactWords; }
+
+hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* d_chunk_counts, int64_t* d_total,
+                               hipStream_t st) {
+  const int64_t nw = (num_docs + 63) / 64;
+  const int64_t nc = compact_num_chunks(num_docs);
+  hipLaunchKernelGGL(bitset_chunk_count_kernel, dim3((unsigned)nc), dim3(kBlock), 0, st, bits, nw, d_chunk_counts);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, d_chunk_counts, nc, d_total);
+  return hipGetLastError();
+}
+
+hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
+                                 int32_t* out, hipStream_t st) {
+  const int64_t nw = (num_docs + 63) / 64;
+  const int64_t nc = compact_num_chunks(num_docs);
+  hipLaunchKernelGGL(bitset_compact_kernel, dim3((unsigned)nc), dim3(kBlock), 0, st, bits, nw, d_chunk_offsets, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const int32_t* sel, int32_t nsel,
+                                 int64_t num_docs, uint64_t* bitset, hipStream_t st) {
+  if (nsel <= 0) return hipSuccess;
+  hipLaunchKernelGGL(roaring_expand_kernel, dim3((unsigned)nsel), dim3(kBlock), 0, st, inv,
+                     reinterpret_cast<const RoaringContainer*>(conts), sel, num_docs,
+                     reinterpret_cast<unsigned long long*>(bitset));
+  return hipGetLastError();
+}
+
+}  // namespace pamd

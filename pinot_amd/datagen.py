@@ -1,0 +1,71 @@
+"""Synthetic segments for the benchmark, generated on the GPU.
+
+The bench table follows the reference README's AdAnalytics example (daysSinceEpoch, clicks,
+impressions, cost) extended with the column kinds BASELINE.json config 1 names: fixed-bit
+dictionary-encoded columns and raw INT / LONG / DOUBLE columns. Values are drawn on the device,
+dictIds are bit-packed by ``pinot_amd_fwd_pack_dict_ids`` (FixedBitSVForwardIndexWriter) and raw
+values are byte-swapped to Pinot's big-endian layout on the device; the resulting segment files
+are then handed to the normal host staging path, exactly as a server would load them.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import segment as S
+from ._lib import check, lib
+
+DAYS_BASE = 17000          # daysSinceEpoch dictionary values DAYS_BASE .. DAYS_BASE+364
+NUM_DAYS = 365
+NUM_COUNTRIES = 200
+
+
+def _be_bytes(t, itemsize: int) -> bytes:
+    """little-endian device tensor -> big-endian host bytes."""
+    return t.contiguous().view(dtype=__import__("torch").uint8).view(-1, itemsize).flip(1).contiguous().cpu().numpy().tobytes()
+
+
+def _fixed_bit(ids, bits: int) -> bytes:
+    import torch
+    n = ids.numel()
+    nbytes = (n * bits + 7) // 8
+    out = torch.zeros(nbytes + 8, dtype=torch.uint8, device=ids.device)
+    check(lib().pinot_amd_fwd_pack_dict_ids(ids.data_ptr(), n, bits, out.data_ptr(), None), "pack")
+    torch.cuda.synchronize()
+    return out[:nbytes].cpu().numpy().tobytes()
+
+
+def ad_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+    """One immutable segment of the AdAnalytics-style bench table (all columns unsorted)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = num_docs
+    cols = {}
+    # fixed-bit dictionary-encoded dimensions
+    for cname, card, base in (("daysSinceEpoch", NUM_DAYS, DAYS_BASE), ("country", NUM_COUNTRIES, 0)):
+        ids = torch.randint(0, card, (n,), generator=g, device=device, dtype=torch.int32)
+        ids[:card] = torch.arange(card, device=device, dtype=torch.int32)  # every dictionary value present
+        bits = S.num_bits_per_value(card - 1)
+        dvals = np.arange(base, base + card, dtype=np.int32)
+        cols[cname] = S.ColumnBuffers(cname, S.INT, n, True, False, card, bits, _fixed_bit(ids, bits),
+                                      S.dictionary_bytes(dvals, S.INT), None, dvals)
+    # raw metrics
+    clicks = torch.randint(0, 1000, (n,), generator=g, device=device, dtype=torch.int32)
+    impressions = torch.randint(0, 1 << 40, (n,), generator=g, device=device, dtype=torch.int64)
+    cost = torch.rand((n,), generator=g, device=device, dtype=torch.float64) * 100.0
+    for cname, t, st, size in (("clicks", clicks, S.INT, 4), ("impressions", impressions, S.LONG, 8),
+                               ("cost", cost, S.DOUBLE, 8)):
+        cols[cname] = S.ColumnBuffers(cname, st, n, False, fwd=S.raw_fwd_header(n, st) + _be_bytes(t, size))
+    torch.cuda.synchronize()
+    return S.SegmentBuffers(name, n, cols)
+
+
+# The benchmark query: range filter on a fixed-bit column AND on a raw INT column, group by a
+# fixed-bit column, SUM/COUNT/MAX over raw INT/LONG/DOUBLE columns (README AdAnalytics shape).
+BENCH_QUERY = ("SELECT daysSinceEpoch, COUNT(*), SUM(clicks), SUM(impressions), SUM(cost), MAX(cost) FROM adAnalytics "
+               f"WHERE daysSinceEpoch BETWEEN {DAYS_BASE + 100} AND {DAYS_BASE + 300} AND clicks > 100 "
+               "GROUP BY daysSinceEpoch")
+
+# Algorithmic HBM bytes per row of BENCH_QUERY: every referenced column is read once
+# (9-bit daysSinceEpoch + 4 B clicks + 8 B impressions + 8 B cost); group accumulators stay in LDS.
+BENCH_BYTES_PER_ROW = S.num_bits_per_value(NUM_DAYS - 1) / 8.0 + 4 + 8 + 8

@@ -1,0 +1,298 @@
+"""Host-side mirror of pinot-core's server query execution for the HBM-resident hot path.
+
+Class names follow the reference so that tests and callers read like Pinot:
+
+* :class:`ImmutableSegment` — ``ImmutableSegmentLoader.load`` (pinot-segment-local/.../loader/
+  ImmutableSegmentLoader.java): stages a segment's column buffers into HBM through
+  ``pinot_amd_segment_add_column``.
+* :class:`ServerQueryExecutor` — ``ServerQueryExecutorV1Impl.execute`` -> ``InstancePlanMakerImplV2``
+  plan -> per-segment ``AggregationOperator`` / ``GroupByOperator`` -> ``*CombineOperator``
+  (pinot-core/.../query/executor/ServerQueryExecutorV1Impl.java). All segments of the call are
+  executed in one batched device pass.
+* :class:`QueryResult` — ``AggregationGroupByResult`` / ``IntermediateResultsBlock``: per group the
+  intermediate results of every aggregation (AVG as (sum, count)), mergeable across servers.
+
+Every computation goes through libpinot_amd.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import ColumnSpec, PredicateSpec, check, lib
+from .query import QueryContext, parse_sql, reduce_rows
+from .segment import ColumnBuffers, SegmentBuffers, DOUBLE, FLOAT, INT, LONG, STRING
+
+TYPE_CODE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3, STRING: 4}
+ENC_CODE = {"FIXED_BIT": 0, "RAW": 1, "SORTED": 2}
+PRED_CODE = {"EQ": 0, "NOT_EQ": 1, "IN": 2, "NOT_IN": 3, "RANGE": 4}
+AGG_CODE = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4, "AVG": 5}
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+class ImmutableSegment:
+    """A segment whose forward indexes, dictionaries and inverted indexes live in HBM."""
+
+    def __init__(self, buffers: SegmentBuffers):
+        L = lib()
+        self.name = buffers.name
+        self.num_docs = buffers.num_docs
+        self.columns: Dict[str, ColumnBuffers] = {}
+        h = C.c_void_p()
+        check(L.pinot_amd_segment_create(buffers.name.encode(), buffers.num_docs, C.byref(h)), "segment_create")
+        self._h = h
+        for cb in buffers.columns.values():
+            self.add_column(cb)
+
+    def add_column(self, cb: ColumnBuffers) -> None:
+        spec = ColumnSpec()
+        spec.name = cb.name.encode()
+        spec.stored_type = TYPE_CODE[cb.stored_type]
+        spec.encoding = ENC_CODE[cb.encoding]
+        spec.cardinality = cb.cardinality
+        spec.bits_per_element = cb.bits_per_element
+        keep = [cb.fwd, cb.dictionary, cb.inverted]
+        spec.h_fwd = C.cast(C.c_char_p(cb.fwd), C.c_void_p)
+        spec.fwd_size = len(cb.fwd)
+        if cb.dictionary:
+            spec.h_dictionary = C.cast(C.c_char_p(cb.dictionary), C.c_void_p)
+            spec.dictionary_size = len(cb.dictionary)
+        if cb.inverted:
+            spec.h_inverted = C.cast(C.c_char_p(cb.inverted), C.c_void_p)
+            spec.inverted_size = len(cb.inverted)
+        check(lib().pinot_amd_segment_add_column(self._h, C.byref(spec)), f"add_column({cb.name})")
+        del keep
+        self.columns[cb.name] = cb
+
+    @property
+    def handle(self):
+        return self._h
+
+    def device_bytes(self) -> int:
+        return int(lib().pinot_amd_segment_device_bytes(self._h))
+
+    def column_fwd_ptr(self, column: str) -> int:
+        p = lib().pinot_amd_segment_column_fwd(self._h, column.encode())
+        if not p:
+            raise KeyError(column)
+        return int(p)
+
+    def destroy(self) -> None:
+        if self._h:
+            lib().pinot_amd_segment_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def _coerce(value, stored_type: str):
+    if stored_type == STRING:
+        return str(value)
+    if stored_type in (INT, LONG):
+        if isinstance(value, float):
+            if not value.is_integer():
+                raise ValueError(f"non-integral literal {value} for {stored_type} column")
+            value = int(value)
+        if isinstance(value, str):
+            value = int(value)
+        return int(value)
+    return float(value)
+
+
+def _predicate_spec(pred, column: ColumnBuffers, use_inverted: bool, keep: list) -> PredicateSpec:
+    s = PredicateSpec()
+    s.column = pred.column.encode()
+    s.type = PRED_CODE[pred.type]
+    st = column.stored_type
+    s.use_inverted_index = 1 if (use_inverted and column.inverted is not None and pred.type != "RANGE") else 0
+    if pred.type == "RANGE":
+        s.lower_unbounded = 1 if pred.lower is None else 0
+        s.upper_unbounded = 1 if pred.upper is None else 0
+        s.lower_inclusive = 1 if pred.lower_inclusive else 0
+        s.upper_inclusive = 1 if pred.upper_inclusive else 0
+        for side in ("lower", "upper"):
+            v = getattr(pred, side)
+            if v is None:
+                continue
+            v = _coerce(v, st)
+            if st == STRING:
+                b = v.encode()
+                keep.append(b)
+                setattr(s, side + "_s", b)
+            elif st in (INT, LONG):
+                setattr(s, side + "_i", v)
+            else:
+                setattr(s, side + "_d", v)
+        return s
+    vals = [_coerce(v, st) for v in pred.values]
+    s.num_values = len(vals)
+    if st == STRING:
+        arr = (C.c_char_p * len(vals))(*[v.encode() for v in vals])
+        keep.append(arr)
+        s.h_values_s = arr
+    elif st in (INT, LONG):
+        arr = (C.c_int64 * len(vals))(*vals)
+        keep.append(arr)
+        s.h_values_i = arr
+    else:
+        arr = (C.c_double * len(vals))(*vals)
+        keep.append(arr)
+        s.h_values_d = arr
+    return s
+
+
+class QueryResult:
+    """Results of one executed query plan (kept in HBM until fetched)."""
+
+    def __init__(self, handle, qc: QueryContext, agg_slots: List[tuple], key_types: List[str]):
+        self._h = handle
+        self.qc = qc
+        self._agg_slots = agg_slots      # per qc aggregation: ('direct', native_idx) | ('avg', sum_idx)
+        self._key_types = key_types
+
+    def execute_again(self, stream=None) -> None:
+        check(lib().pinot_amd_execute_again(self._h, _stream_handle(stream)), "execute_again")
+
+    def num_docs_matched(self) -> int:
+        out = C.c_int64()
+        check(lib().pinot_amd_result_num_docs_matched(self._h, C.byref(out)), "num_docs_matched")
+        return out.value
+
+    def last_kernel_ms(self) -> float:
+        out = C.c_double()
+        check(lib().pinot_amd_result_last_kernel_ms(self._h, C.byref(out)), "last_kernel_ms")
+        return out.value
+
+    def accumulators(self):
+        """(ops, num_keys, [device pointers]) of the dense accumulators for a cross-GPU merge."""
+        n = C.c_int32()
+        nk = C.c_int64()
+        check(lib().pinot_amd_result_accumulators(self._h, C.byref(n), C.byref(nk), None, None), "accumulators")
+        ptrs = (C.c_void_p * n.value)()
+        ops = (C.c_int32 * n.value)()
+        check(lib().pinot_amd_result_accumulators(self._h, C.byref(n), C.byref(nk), ptrs, ops), "accumulators")
+        return list(ops), nk.value, [int(p) for p in ptrs]
+
+    def groups(self) -> Dict[tuple, list]:
+        """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation."""
+        L = lib()
+        ng = C.c_int64()
+        check(L.pinot_amd_result_num_groups(self._h, C.byref(ng)), "num_groups")
+        n = max(ng.value, 1)
+        nk = len(self.qc.group_by)
+        nnat = max(len(self._native_aggs), 1)
+        keys = np.zeros(n * max(nk, 1), dtype=np.int64)
+        vals = np.zeros(n * nnat, dtype=np.float64)
+        vals_i = np.zeros(n * nnat, dtype=np.int64)
+        got = C.c_int64()
+        check(L.pinot_amd_result_fetch(self._h, n, keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                       vals.ctypes.data_as(C.POINTER(C.c_double)),
+                                       vals_i.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(got)), "fetch")
+        out = {}
+        for g in range(got.value):
+            key = []
+            for j in range(nk):
+                raw = int(keys[g * nk + j])
+                t = self._key_types[j]
+                if t == STRING:
+                    key.append(L.pinot_amd_result_string_key(self._h, j, raw).decode())
+                elif t in (FLOAT, DOUBLE):
+                    key.append(float(np.int64(raw).view(np.float64)))
+                else:
+                    key.append(raw)
+            parts = []
+            for a, slot in zip(self.qc.aggregations, self._agg_slots):
+                if slot[0] == "avg":
+                    s = vals[g * nnat + slot[1]]
+                    c = vals_i[g * nnat + slot[2]]
+                    parts.append((float(s), int(c)))
+                elif a.func in ("COUNT", "SUMLONG"):
+                    parts.append(int(vals_i[g * nnat + slot[1]]))
+                else:
+                    parts.append(float(vals[g * nnat + slot[1]]))
+            out[tuple(key)] = parts
+        return out
+
+    def rows(self) -> List[tuple]:
+        return reduce_rows(self.qc, self.groups())
+
+    def destroy(self) -> None:
+        if self._h:
+            lib().pinot_amd_result_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+class ServerQueryExecutor:
+    """Compiles a QueryContext and runs it over a list of HBM-resident segments."""
+
+    def __init__(self, use_inverted_index: bool = True):
+        self.use_inverted_index = use_inverted_index
+
+    def execute(self, query, segments: Sequence[ImmutableSegment], stream=None) -> QueryResult:
+        qc = parse_sql(query) if isinstance(query, str) else query
+        if not segments:
+            raise ValueError("no segments")
+        L = lib()
+        first = segments[0]
+        qh = C.c_void_p()
+        check(L.pinot_amd_query_create(C.byref(qh)), "query_create")
+        keep: list = []
+        try:
+            for ci, clause in enumerate(qc.cnf):
+                for pred, neg in clause:
+                    col = first.columns.get(pred.column)
+                    if col is None:
+                        raise _lib.PinotAmdError(f"unknown column {pred.column!r} in segment {first.name}")
+                    spec = _predicate_spec(pred, col, self.use_inverted_index, keep)
+                    check(L.pinot_amd_query_add_predicate(qh, ci, C.byref(spec), 1 if neg else 0), "add_predicate")
+            for g in qc.group_by:
+                check(L.pinot_amd_query_add_group_by(qh, g.encode()), "add_group_by")
+            check(L.pinot_amd_query_set_num_groups_limit(qh, qc.num_groups_limit), "set_num_groups_limit")
+            native = []
+            agg_slots = []
+
+            def add(func, column):
+                key = (func, column)
+                if key in native:
+                    return native.index(key)
+                idx = C.c_int32()
+                check(L.pinot_amd_query_add_aggregation(qh, AGG_CODE[func], column.encode(), C.byref(idx)),
+                      f"add_aggregation({func})")
+                native.append(key)
+                return idx.value
+
+            for a in qc.aggregations:
+                if a.func == "AVG":
+                    agg_slots.append(("avg", add("SUM", a.column), add("COUNT", "*")))
+                else:
+                    agg_slots.append(("direct", add(a.func, a.column)))
+            if not qc.aggregations and qc.group_by:
+                add("COUNT", "*")  # DISTINCT-style group-by still needs the group presence count
+            arr = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
+            rh = C.c_void_p()
+            check(L.pinot_amd_execute(qh, arr, len(segments), _stream_handle(stream), C.byref(rh)), "execute")
+        finally:
+            L.pinot_amd_query_destroy(qh)
+        key_types = [first.columns[g].stored_type for g in qc.group_by]
+        res = QueryResult(rh, qc, agg_slots, key_types)
+        res._native_aggs = native
+        return res

@@ -1,0 +1,380 @@
+"""QueryContext for the segment-execution path: a small SQL front end and the filter's CNF form.
+
+Mirrors the pieces of pinot-core's request context that the hot path consumes
+(pinot-common/.../request/context/predicate/*Predicate.java, FilterContext.java,
+pinot-core/.../query/request/context/QueryContext.java): aggregation functions, GROUP BY
+expressions, the filter tree, ORDER BY / LIMIT for the final reduce, and the numGroupsLimit
+query option. Only the SQL this path executes is accepted (identifiers, numeric/string
+literals, comparisons, BETWEEN, [NOT] IN, AND/OR/NOT); anything else raises ValueError.
+"""
+from __future__ import annotations
+
+import dataclasses
+import re
+from typing import List, Optional, Sequence, Tuple
+
+AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG")
+DEFAULT_GROUP_BY_LIMIT = 10          # Pinot's default LIMIT for group-by results
+DEFAULT_NUM_GROUPS_LIMIT = 100_000   # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
+
+
+@dataclasses.dataclass(frozen=True)
+class Predicate:
+    """EQ / NOT_EQ / IN / NOT_IN / RANGE on one column (RangePredicate: None bound = UNBOUNDED)."""
+    type: str
+    column: str
+    values: Tuple = ()
+    lower: object = None
+    upper: object = None
+    lower_inclusive: bool = True
+    upper_inclusive: bool = True
+
+    def negated(self) -> "Predicate":
+        flip = {"EQ": "NOT_EQ", "NOT_EQ": "EQ", "IN": "NOT_IN", "NOT_IN": "IN"}
+        if self.type in flip:
+            return dataclasses.replace(self, type=flip[self.type])
+        raise NotImplementedError  # RANGE negation is represented with a negate flag
+
+
+@dataclasses.dataclass
+class FilterContext:
+    type: str  # AND | OR | NOT | PREDICATE
+    children: List["FilterContext"] = dataclasses.field(default_factory=list)
+    predicate: Optional[Predicate] = None
+
+    @staticmethod
+    def pred(p: Predicate) -> "FilterContext":
+        return FilterContext("PREDICATE", predicate=p)
+
+    @staticmethod
+    def and_(*c) -> "FilterContext":
+        return FilterContext("AND", list(c))
+
+    @staticmethod
+    def or_(*c) -> "FilterContext":
+        return FilterContext("OR", list(c))
+
+    @staticmethod
+    def not_(c) -> "FilterContext":
+        return FilterContext("NOT", [c])
+
+
+Leaf = Tuple[Predicate, bool]  # (predicate, negate)
+
+
+def to_cnf(f: Optional[FilterContext]) -> List[List[Leaf]]:
+    """AND of OR-clauses of (predicate, negate) leaves; NOT is pushed to the leaves (De Morgan)."""
+    if f is None:
+        return []
+
+    def nnf(node: FilterContext, neg: bool):
+        if node.type == "PREDICATE":
+            return ("LEAF", (node.predicate, neg))
+        if node.type == "NOT":
+            return nnf(node.children[0], not neg)
+        op = node.type
+        if neg:
+            op = "OR" if op == "AND" else "AND"
+        return (op, [nnf(c, neg) for c in node.children])
+
+    def cnf(n) -> List[List[Leaf]]:
+        if n[0] == "LEAF":
+            return [[n[1]]]
+        parts = [cnf(c) for c in n[1]]
+        if n[0] == "AND":
+            out = []
+            for p in parts:
+                out.extend(p)
+            return out
+        # OR: distribute
+        acc = [[]]
+        for p in parts:
+            acc = [a + b for a in acc for b in p]
+        return acc
+
+    return cnf(nnf(f, False))
+
+
+@dataclasses.dataclass
+class Aggregation:
+    func: str          # COUNT SUM MIN MAX AVG SUMLONG
+    column: str        # "*" for COUNT(*)
+    alias: Optional[str] = None
+
+    @property
+    def name(self) -> str:
+        return self.alias or f"{self.func.lower()}({self.column})"
+
+
+@dataclasses.dataclass
+class QueryContext:
+    table: str
+    aggregations: List[Aggregation]
+    group_by: List[str]
+    filter: Optional[FilterContext]
+    order_by: List[Tuple[str, bool]]   # (expression or alias, ascending)
+    limit: int
+    select_columns: List[str]           # plain columns in the SELECT list (group-by outputs)
+    num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT
+
+    @property
+    def cnf(self) -> List[List[Leaf]]:
+        return to_cnf(self.filter)
+
+
+# ---------------------------------------------------------------------------------------- parser
+_TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+\.\d*(?:[eE][-+]?\d+)?|-?\d+(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')"
+                    r"|(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
+
+
+def _tokenize(sql: str):
+    pos, out = 0, []
+    sql = sql.strip().rstrip(";")
+    while pos < len(sql):
+        m = _TOKEN.match(sql, pos)
+        if not m or m.end() == pos:
+            if sql[pos:].strip() == "":
+                break
+            raise ValueError(f"cannot tokenize at: {sql[pos:pos + 20]!r}")
+        pos = m.end()
+        if m.group("num") is not None:
+            t = m.group("num")
+            out.append(("num", float(t) if any(ch in t for ch in ".eE") else int(t)))
+        elif m.group("str") is not None:
+            out.append(("str", m.group("str")[1:-1].replace("''", "'")))
+        elif m.group("op") is not None:
+            out.append(("op", m.group("op")))
+        else:
+            out.append(("id", m.group("id")))
+    return out
+
+
+class _Parser:
+    def __init__(self, sql: str):
+        self.t = _tokenize(sql)
+        self.i = 0
+
+    def peek(self, k=0):
+        return self.t[self.i + k] if self.i + k < len(self.t) else ("eof", None)
+
+    def kw(self, *words) -> bool:
+        for k, w in enumerate(words):
+            tok = self.peek(k)
+            if tok[0] != "id" or tok[1].upper() != w:
+                return False
+        return True
+
+    def eat_kw(self, *words):
+        if not self.kw(*words):
+            raise ValueError(f"expected {' '.join(words)} at token {self.peek()}")
+        self.i += len(words)
+
+    def eat_op(self, op):
+        tok = self.peek()
+        if tok != ("op", op):
+            raise ValueError(f"expected {op!r} at token {tok}")
+        self.i += 1
+
+    def ident(self) -> str:
+        tok = self.peek()
+        if tok[0] != "id":
+            raise ValueError(f"expected identifier at {tok}")
+        self.i += 1
+        return tok[1]
+
+    def literal(self):
+        tok = self.peek()
+        if tok[0] not in ("num", "str"):
+            raise ValueError(f"expected literal at {tok}")
+        self.i += 1
+        return tok[1]
+
+    # -- grammar --
+    def query(self) -> QueryContext:
+        self.eat_kw("SELECT")
+        aggs, cols = [], []
+        while True:
+            tok = self.peek()
+            if tok[0] == "id" and tok[1].upper() in AGG_FUNCS and self.peek(1) == ("op", "("):
+                func = tok[1].upper()
+                self.i += 2
+                if self.peek() == ("op", "*"):
+                    self.i += 1
+                    col = "*"
+                else:
+                    col = self.ident()
+                self.eat_op(")")
+                alias = None
+                if self.kw("AS"):
+                    self.i += 1
+                    alias = self.ident()
+                aggs.append(Aggregation(func, col, alias))
+            else:
+                cols.append(self.ident())
+            if self.peek() == ("op", ","):
+                self.i += 1
+                continue
+            break
+        self.eat_kw("FROM")
+        table = self.ident()
+        flt = None
+        if self.kw("WHERE"):
+            self.i += 1
+            flt = self.expr()
+        group_by = []
+        if self.kw("GROUP", "BY"):
+            self.i += 2
+            group_by.append(self.ident())
+            while self.peek() == ("op", ","):
+                self.i += 1
+                group_by.append(self.ident())
+        order = []
+        if self.kw("ORDER", "BY"):
+            self.i += 2
+            while True:
+                order.append(self.order_item())
+                if self.peek() != ("op", ","):
+                    break
+                self.i += 1
+        limit = DEFAULT_GROUP_BY_LIMIT
+        if self.kw("LIMIT"):
+            self.i += 1
+            limit = int(self.literal())
+        if self.peek()[0] != "eof":
+            raise ValueError(f"unexpected trailing token {self.peek()}")
+        return QueryContext(table, aggs, group_by, flt, order, limit, cols)
+
+    def order_item(self):
+        tok = self.peek()
+        if tok[0] == "id" and tok[1].upper() in AGG_FUNCS and self.peek(1) == ("op", "("):
+            func = tok[1].upper()
+            self.i += 2
+            col = "*" if self.peek() == ("op", "*") else self.peek()[1]
+            self.i += 1
+            self.eat_op(")")
+            expr = f"{func.lower()}({col})"
+        else:
+            expr = self.ident()
+        asc = True
+        if self.kw("DESC"):
+            self.i += 1
+            asc = False
+        elif self.kw("ASC"):
+            self.i += 1
+        return (expr, asc)
+
+    def expr(self) -> FilterContext:
+        node = self.and_expr()
+        children = [node]
+        while self.kw("OR"):
+            self.i += 1
+            children.append(self.and_expr())
+        return children[0] if len(children) == 1 else FilterContext.or_(*children)
+
+    def and_expr(self) -> FilterContext:
+        children = [self.not_expr()]
+        while self.kw("AND"):
+            self.i += 1
+            children.append(self.not_expr())
+        return children[0] if len(children) == 1 else FilterContext.and_(*children)
+
+    def not_expr(self) -> FilterContext:
+        if self.kw("NOT"):
+            self.i += 1
+            return FilterContext.not_(self.not_expr())
+        if self.peek() == ("op", "("):
+            self.i += 1
+            e = self.expr()
+            self.eat_op(")")
+            return e
+        return self.comparison()
+
+    def comparison(self) -> FilterContext:
+        col = self.ident()
+        if self.kw("NOT", "IN") or self.kw("IN"):
+            neg = self.kw("NOT")
+            self.i += 2 if neg else 1
+            self.eat_op("(")
+            vals = [self.literal()]
+            while self.peek() == ("op", ","):
+                self.i += 1
+                vals.append(self.literal())
+            self.eat_op(")")
+            return FilterContext.pred(Predicate("NOT_IN" if neg else "IN", col, tuple(vals)))
+        if self.kw("NOT", "BETWEEN") or self.kw("BETWEEN"):
+            neg = self.kw("NOT")
+            self.i += 2 if neg else 1
+            lo = self.literal()
+            self.eat_kw("AND")
+            hi = self.literal()
+            p = FilterContext.pred(Predicate("RANGE", col, lower=lo, upper=hi))
+            return FilterContext.not_(p) if neg else p
+        tok = self.peek()
+        if tok[0] != "op":
+            raise ValueError(f"expected comparison operator at {tok}")
+        self.i += 1
+        v = self.literal()
+        op = tok[1]
+        if op == "=":
+            return FilterContext.pred(Predicate("EQ", col, (v,)))
+        if op in ("<>", "!="):
+            return FilterContext.pred(Predicate("NOT_EQ", col, (v,)))
+        if op == "<":
+            return FilterContext.pred(Predicate("RANGE", col, upper=v, upper_inclusive=False))
+        if op == "<=":
+            return FilterContext.pred(Predicate("RANGE", col, upper=v, upper_inclusive=True))
+        if op == ">":
+            return FilterContext.pred(Predicate("RANGE", col, lower=v, lower_inclusive=False))
+        if op == ">=":
+            return FilterContext.pred(Predicate("RANGE", col, lower=v, lower_inclusive=True))
+        raise ValueError(f"unsupported operator {op}")
+
+
+def parse_sql(sql: str) -> QueryContext:
+    """Compile a Pinot SQL query of the supported subset into a QueryContext."""
+    return _Parser(sql).query()
+
+
+# ---------------------------------------------------------------------------------------- reduce
+def final_value(func: str, partial):
+    """AggregationFunction.extractFinalResult: AVG -> sum / count, others unchanged."""
+    if func == "AVG":
+        s, c = partial
+        return s / c if c else float("-inf")
+    return partial
+
+
+def merge_partial(func: str, a, b):
+    """AggregationFunction.merge (used by the combine and broker reduce)."""
+    if func in ("COUNT", "SUM", "SUMLONG"):
+        return a + b
+    if func == "MIN":
+        return min(a, b)
+    if func == "MAX":
+        return max(a, b)
+    if func == "AVG":
+        return (a[0] + b[0], a[1] + b[1])
+    raise ValueError(func)
+
+
+def reduce_rows(qc: QueryContext, groups: dict) -> List[tuple]:
+    """Broker reduce for group-by: final results, ORDER BY, LIMIT (default 10).
+
+    groups: key tuple -> list of per-aggregation partials. Returns rows of
+    (group values..., final aggregation values...).
+    """
+    rows = []
+    for key, parts in groups.items():
+        rows.append(tuple(key) + tuple(final_value(a.func, p) for a, p in zip(qc.aggregations, parts)))
+    names = list(qc.group_by) + [a.name for a in qc.aggregations]
+    exprs = list(qc.group_by) + [f"{a.func.lower()}({a.column})" for a in qc.aggregations]
+    for expr, asc in reversed(qc.order_by):
+        e = expr.lower()
+        idx = None
+        for i, (n, x) in enumerate(zip(names, exprs)):
+            if e in (n.lower(), x.lower()):
+                idx = i
+        if idx is None:
+            raise ValueError(f"ORDER BY {expr} not in select list")
+        rows.sort(key=lambda r: r[idx], reverse=not asc)
+    return rows[: qc.limit]

@@ -1,0 +1,340 @@
+"""Immutable-segment column buffers in Pinot's on-disk byte formats (numpy, host side).
+
+This module produces and parses the exact bytes a Pinot server mmaps as
+``PinotDataBuffer``s for one immutable segment, so that the HBM stager and the
+CPU oracle see the same buffers the reference's readers see:
+
+* dictionary-encoded single-value forward index, bit packed MSB-first, big-endian
+  (writer: ``FixedBitSVForwardIndexWriter`` / ``PinotDataBitSet.writeInt``,
+  pinot-segment-local/.../io/util/PinotDataBitSet.java:143-170; reader:
+  ``FixedBitSVForwardIndexReaderV2``, .../readers/forward/FixedBitSVForwardIndexReaderV2.java:33);
+* sorted forward index: one big-endian ``(minDocId, maxDocId)`` int pair per dictId
+  (.../creator/impl/fwd/SingleValueSortedForwardIndexCreator.java:53-70, read by
+  ``SortedIndexReaderImpl``);
+* raw fixed-byte chunk forward index, PASS_THROUGH chunks, header of 7 big-endian ints
+  plus chunk offsets (.../io/writer/impl/BaseChunkForwardIndexWriter.java:131-165,
+  read by ``FixedBytePower2ChunkSVForwardIndexReader`` / ``BaseChunkForwardIndexReader``
+  .../readers/forward/BaseChunkForwardIndexReader.java:60-105);
+* sorted dictionaries of big-endian fixed-width values, strings padded with NUL
+  (``IntDictionary``/``LongDictionary``/``FloatDictionary``/``DoubleDictionary``/``StringDictionary``);
+* bitmap inverted index: (cardinality+1) big-endian absolute offsets followed by
+  RoaringBitmap portable serialisations
+  (.../creator/impl/inv/BitmapInvertedIndexWriter.java:37-52, read by
+  ``BitmapInvertedIndexReader`` .../readers/BitmapInvertedIndexReader.java:44-60).
+
+RoaringBitmap (org.roaringbitmap:RoaringBitmap 1.6.14, pom.xml:214) is a third-party
+dependency that is not vendored in the reference; its portable serialisation format
+is restated here (cookie 12346 = no run containers, 12347 = with run containers).
+
+Nothing here runs on the GPU; this is segment *creation* (test and bench input)
+plus format parsing shared by the stager.
+"""
+from __future__ import annotations
+
+import dataclasses
+import struct
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+# FieldSpec.DataType stored types handled on the hot path
+INT, LONG, FLOAT, DOUBLE, STRING = "INT", "LONG", "FLOAT", "DOUBLE", "STRING"
+_NP_BE = {INT: ">i4", LONG: ">i8", FLOAT: ">f4", DOUBLE: ">f8"}
+_NP_LE = {INT: "<i4", LONG: "<i8", FLOAT: "<f4", DOUBLE: "<f8"}
+VALUE_SIZE = {INT: 4, LONG: 8, FLOAT: 4, DOUBLE: 8}
+
+# ChunkCompressionType (pinot-segment-spi/.../compression/ChunkCompressionType.java:22)
+PASS_THROUGH = 0
+
+# Default null values (FieldSpec.DEFAULT_*_NULL_VALUE_OF_*), used when ingesting nulls
+DEFAULT_DIMENSION_NULL = {INT: np.iinfo(np.int32).min, LONG: np.iinfo(np.int64).min,
+                          FLOAT: float("-inf"), DOUBLE: float("-inf"), STRING: "null"}
+DEFAULT_METRIC_NULL = {INT: 0, LONG: 0, FLOAT: 0.0, DOUBLE: 0.0, STRING: "null"}
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue (PinotDataBitSet.java:61-72): at least one bit."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
+
+
+# --------------------------------------------------------------------------- fixed-bit
+def pack_fixed_bit(values: np.ndarray, bits: int) -> bytes:
+    """Bit-pack non-negative ints MSB-first into a big-endian bit stream.
+
+    Same bytes as ``FixedBitSVForwardIndexWriter`` (value i occupies stream bits
+    [i*bits, (i+1)*bits), bit 0 = MSB of byte 0; PinotDataBitSet.java:143-170).
+    The buffer is sized ceil(n*bits/8) bytes like the writer's file.
+    """
+    v = np.ascontiguousarray(values, dtype=np.uint64)
+    if v.size and (int(v.max()) >> bits) != 0:
+        raise ValueError(f"value does not fit in {bits} bits")
+    n = v.size
+    out = np.zeros((n * bits + 7) // 8, dtype=np.uint8)
+    step = 1 << 20
+    for s in range(0, n, step):  # bounded temporaries
+        e = min(n, s + step)
+        shifts = np.arange(bits - 1, -1, -1, dtype=np.uint64)
+        bitmat = ((v[s:e, None] >> shifts) & np.uint64(1)).astype(np.uint8).ravel()
+        first_bit = s * bits
+        # s is a multiple of 2^20, so first_bit is a multiple of 8
+        packed = np.packbits(bitmat)
+        out[first_bit // 8: first_bit // 8 + packed.size] |= packed
+    return out.tobytes()
+
+
+def unpack_fixed_bit(buf: bytes, bits: int, n: int) -> np.ndarray:
+    """Vectorised inverse of :func:`pack_fixed_bit` (host helper, not the oracle)."""
+    a = np.frombuffer(buf, dtype=np.uint8)
+    allbits = np.unpackbits(a)[: n * bits].reshape(n, bits).astype(np.int64)
+    w = (1 << np.arange(bits - 1, -1, -1, dtype=np.int64))
+    return (allbits * w).sum(axis=1).astype(np.int32)
+
+
+# --------------------------------------------------------------------------- sorted fwd
+def sorted_fwd_bytes(dict_ids: np.ndarray, cardinality: int) -> bytes:
+    """SingleValueSortedForwardIndexCreator: (minDocId, maxDocId) per dictId, big-endian ints."""
+    d = np.asarray(dict_ids, dtype=np.int64)
+    if d.size > 1 and np.any(np.diff(d) < 0):
+        raise ValueError("column is not sorted")
+    pairs = np.empty((cardinality, 2), dtype=">i4")
+    pairs[:, 0] = np.iinfo(np.int32).max
+    pairs[:, 1] = np.iinfo(np.int32).min
+    if d.size:
+        ids, first = np.unique(d, return_index=True)
+        last = np.r_[first[1:], d.size] - 1
+        pairs[ids, 0] = first
+        pairs[ids, 1] = last
+    return pairs.tobytes()
+
+
+# --------------------------------------------------------------------------- raw fwd
+RAW_HEADER_INTS = 7
+
+
+def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:
+    """FixedByteChunkForwardIndexWriter with PASS_THROUGH chunks.
+
+    Header (BaseChunkForwardIndexWriter.java:131-165): version, numChunks,
+    numDocsPerChunk, sizeOfEntry, totalDocs, compressionType, dataHeaderStart, then
+    one chunk offset per chunk (int for v2, long for v3+), then the chunks. v4 rounds
+    docsPerChunk up to a power of two (FixedByteChunkForwardIndexWriter.java:90-96).
+    Values are big-endian (java.nio.ByteBuffer default order).
+    """
+    data = np.ascontiguousarray(values).astype(_NP_BE[stored_type]).tobytes()
+    return raw_fwd_header(int(values.size), stored_type, version, docs_per_chunk) + data
+
+
+def raw_fwd_header(n: int, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:
+    """Header + chunk-offset table of a PASS_THROUGH FixedByteChunkForwardIndexWriter file of n values."""
+    if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
+        docs_per_chunk = 1 << (docs_per_chunk - 1).bit_length()
+    size = VALUE_SIZE[stored_type]
+    num_chunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version == 2 else 8
+    header_size = RAW_HEADER_INTS * 4 + num_chunks * off_size
+    hdr = struct.pack(">7i", version, num_chunks, docs_per_chunk, size, n, PASS_THROUGH, RAW_HEADER_INTS * 4)
+    chunk_bytes = docs_per_chunk * size
+    offs = np.arange(num_chunks, dtype=np.int64) * chunk_bytes + header_size
+    # the last chunk is written with only its present bytes (writeChunk flips the buffer)
+    return hdr + offs.astype(">i4" if off_size == 4 else ">i8").tobytes()
+
+
+@dataclasses.dataclass
+class RawFwdHeader:
+    version: int
+    num_chunks: int
+    docs_per_chunk: int
+    size_of_entry: int
+    total_docs: int
+    compression: int
+    data_header_start: int
+    raw_data_start: int
+
+
+def parse_raw_fwd_header(buf: bytes) -> RawFwdHeader:
+    """BaseChunkForwardIndexReader constructor (BaseChunkForwardIndexReader.java:60-105)."""
+    version, num_chunks, dpc, size = struct.unpack_from(">4i", buf, 0)
+    if version > 1:
+        total, comp, dhs = struct.unpack_from(">3i", buf, 16)
+    else:
+        total, comp, dhs = -1, 1, 16
+    off_size = 4 if version <= 2 else 8
+    return RawFwdHeader(version, num_chunks, dpc, size, total, comp, dhs, dhs + num_chunks * off_size)
+
+
+# --------------------------------------------------------------------------- dictionary
+def dictionary_bytes(sorted_values, stored_type: str) -> bytes:
+    """Fixed-width big-endian dictionary buffer (strings padded with NUL to the longest UTF-8 entry)."""
+    if stored_type == STRING:
+        enc = [s.encode("utf-8") for s in sorted_values]
+        width = max([len(e) for e in enc] + [1])
+        return b"".join(e.ljust(width, b"\0") for e in enc)
+    return np.asarray(sorted_values).astype(_NP_BE[stored_type]).tobytes()
+
+
+def decode_dictionary(buf: bytes, stored_type: str, cardinality: int) -> np.ndarray:
+    if stored_type == STRING:
+        width = len(buf) // max(cardinality, 1)
+        return np.array([buf[i * width:(i + 1) * width].rstrip(b"\0").decode("utf-8") for i in range(cardinality)],
+                        dtype=object)
+    return np.frombuffer(buf, dtype=_NP_BE[stored_type], count=cardinality).astype(_NP_LE[stored_type])
+
+
+def _java_string_key(s: str):
+    # String.compareTo compares UTF-16 code units
+    return s.encode("utf-16-be")
+
+
+def build_dictionary(values: np.ndarray, stored_type: str):
+    """Sorted dictionary + dictIds (SegmentDictionaryCreator sorts the unique values)."""
+    if stored_type == STRING:
+        uniq = sorted(set(values.tolist()), key=_java_string_key)
+        index = {v: i for i, v in enumerate(uniq)}
+        ids = np.fromiter((index[v] for v in values.tolist()), dtype=np.int32, count=len(values))
+        return np.array(uniq, dtype=object), ids
+    uniq, ids = np.unique(np.asarray(values), return_inverse=True)
+    return uniq.astype(_NP_LE[stored_type]), ids.astype(np.int32)
+
+
+# --------------------------------------------------------------------------- roaring
+ROARING_COOKIE_NO_RUN = 12346
+ROARING_COOKIE = 12347
+ROARING_NO_OFFSET_THRESHOLD = 4
+ARRAY_MAX = 4096
+
+
+def roaring_serialize(doc_ids: np.ndarray, run_optimize: bool = True) -> bytes:
+    """RoaringBitmap.serialize (portable format) of a sorted unique set of docIds.
+
+    Containers: array (cardinality <= 4096, sorted u16), bitmap (1024 u64 words) or,
+    when ``run_optimize`` and smaller, run ((start, length-1) u16 pairs), as
+    RoaringBitmap.runOptimize would choose. All little-endian.
+    """
+    d = np.asarray(doc_ids, dtype=np.int64)
+    keys = np.unique(d >> 16) if d.size else np.zeros(0, np.int64)
+    conts = []
+    for k in keys.tolist():
+        low = (d[(d >> 16) == k] & 0xFFFF).astype(np.int64)
+        card = low.size
+        starts = np.r_[True, np.diff(low) != 1]
+        run_starts = low[starts]
+        run_ends = np.r_[low[np.nonzero(starts)[0][1:] - 1], low[-1]]
+        nruns = run_starts.size
+        run_size = 2 + 4 * nruns
+        std_size = 2 * card if card <= ARRAY_MAX else 8192
+        if run_optimize and run_size < std_size:
+            body = struct.pack("<H", nruns) + np.stack([run_starts, run_ends - run_starts], 1).astype("<u2").tobytes()
+            conts.append((k, card, "run", body))
+        elif card <= ARRAY_MAX:
+            conts.append((k, card, "array", low.astype("<u2").tobytes()))
+        else:
+            words = np.zeros(1024, dtype=np.uint64)
+            np.bitwise_or.at(words, low >> 6, np.uint64(1) << (low & 63).astype(np.uint64))
+            conts.append((k, card, "bitmap", words.astype("<u8").tobytes()))
+    size = len(conts)
+    has_run = any(c[2] == "run" for c in conts)
+    out = bytearray()
+    if has_run:
+        out += struct.pack("<i", ROARING_COOKIE | ((size - 1) << 16))
+        runbits = bytearray((size + 7) // 8)
+        for i, c in enumerate(conts):
+            if c[2] == "run":
+                runbits[i // 8] |= 1 << (i % 8)
+        out += runbits
+    else:
+        out += struct.pack("<ii", ROARING_COOKIE_NO_RUN, size)
+    for k, card, _, _ in conts:
+        out += struct.pack("<HH", k, card - 1)
+    if (not has_run) or size >= ROARING_NO_OFFSET_THRESHOLD:
+        pos = len(out) + 4 * size
+        for _, _, _, body in conts:
+            out += struct.pack("<i", pos)
+            pos += len(body)
+    for _, _, _, body in conts:
+        out += body
+    return bytes(out)
+
+
+def inverted_index_bytes(dict_ids: np.ndarray, cardinality: int) -> bytes:
+    """BitmapInvertedIndexWriter layout: (cardinality+1) BE absolute offsets, then bitmaps."""
+    d = np.asarray(dict_ids, dtype=np.int64)
+    order = np.argsort(d, kind="stable")
+    sd = d[order]
+    bounds = np.searchsorted(sd, np.arange(cardinality + 1))
+    bitmaps = [roaring_serialize(np.sort(order[bounds[i]:bounds[i + 1]])) for i in range(cardinality)]
+    pos = (cardinality + 1) * 4
+    offs = [pos]
+    for b in bitmaps:
+        pos += len(b)
+        offs.append(pos)
+    return struct.pack(">%dI" % (cardinality + 1), *offs) + b"".join(bitmaps)
+
+
+# --------------------------------------------------------------------------- segment
+@dataclasses.dataclass
+class ColumnBuffers:
+    """One column of an immutable segment: metadata + the PinotDataBuffers the server maps."""
+    name: str
+    stored_type: str
+    num_docs: int
+    has_dictionary: bool
+    is_sorted: bool = False
+    cardinality: int = 0
+    bits_per_element: int = 0
+    fwd: bytes = b""                     # forward index buffer (fixed-bit | sorted pairs | raw chunk file)
+    dictionary: bytes = b""              # dictionary buffer (dict-encoded columns)
+    inverted: Optional[bytes] = None     # bitmap inverted index buffer
+    dict_values: Optional[np.ndarray] = None  # decoded dictionary (host convenience)
+
+    @property
+    def encoding(self) -> str:
+        if not self.has_dictionary:
+            return "RAW"
+        return "SORTED" if self.is_sorted else "FIXED_BIT"
+
+
+@dataclasses.dataclass
+class SegmentBuffers:
+    name: str
+    num_docs: int
+    columns: Dict[str, ColumnBuffers]
+
+    def column(self, name: str) -> ColumnBuffers:
+        return self.columns[name]
+
+
+def build_column(name: str, values, stored_type: str, dictionary: bool = True, inverted: bool = False,
+                 detect_sorted: bool = True, raw_version: int = 4) -> ColumnBuffers:
+    """Create one column's buffers the way SegmentColumnarIndexCreator would for an SV column."""
+    vals = np.asarray(values, dtype=object if stored_type == STRING else _NP_LE[stored_type])
+    n = int(vals.size)
+    if not dictionary:
+        if stored_type == STRING:
+            raise NotImplementedError("raw STRING forward index is outside the hot path")
+        return ColumnBuffers(name, stored_type, n, False, fwd=raw_fwd_bytes(vals, stored_type, raw_version))
+    dvals, ids = build_dictionary(vals, stored_type)
+    card = len(dvals)
+    is_sorted = bool(detect_sorted and (n < 2 or np.all(np.diff(ids.astype(np.int64)) >= 0)))
+    bits = num_bits_per_value(card - 1)
+    fwd = sorted_fwd_bytes(ids, card) if is_sorted else pack_fixed_bit(ids, bits)
+    inv = inverted_index_bytes(ids, card) if inverted else None
+    return ColumnBuffers(name, stored_type, n, True, is_sorted, card, bits, fwd, dictionary_bytes(dvals, stored_type),
+                         inv, dvals)
+
+
+def build_segment(name: str, columns: Dict[str, tuple]) -> SegmentBuffers:
+    """columns: name -> (values, stored_type, kwargs-dict)."""
+    cols = {}
+    n = None
+    for cname, spec in columns.items():
+        values, stype = spec[0], spec[1]
+        kw = spec[2] if len(spec) > 2 else {}
+        c = build_column(cname, values, stype, **kw)
+        if n is None:
+            n = c.num_docs
+        elif c.num_docs != n:
+            raise ValueError("ragged columns")
+        cols[cname] = c
+    return SegmentBuffers(name, n or 0, cols)

@@ -1,0 +1,56 @@
+"""Shared test helpers: golden segment construction and random segment generators."""
+import json
+import os
+
+import numpy as np
+
+from pinot_amd.segment import build_segment, DOUBLE, FLOAT, INT, LONG, STRING
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# BaseSingleValueQueriesTest.java:62-80: schema + inverted index columns
+SV_COLUMNS = [("column1", INT), ("column3", INT), ("column5", STRING), ("column6", INT), ("column7", INT),
+              ("column9", INT), ("column11", STRING), ("column12", STRING), ("column17", INT), ("column18", INT),
+              ("daysSinceEpoch", INT)]
+SV_INVERTED = {"column6", "column7", "column11", "column17", "column18"}
+SV_FILTER = (" WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 1000000000 AND column5 = 'gFuH'"
+             " AND (column6 < 500000000 OR column11 NOT IN ('t', 'P')) AND daysSinceEpoch = 126164076")
+
+
+def load_expected():
+    with open(os.path.join(GOLDEN, "sv_queries_expected.json")) as f:
+        return json.load(f)
+
+
+def sv_segment(name="testTable_126164076_167572854"):
+    data = np.load(os.path.join(GOLDEN, "test_data_sv.npz"), allow_pickle=False)
+    cols = {}
+    for c, t in SV_COLUMNS:
+        v = data[c]
+        if t == STRING:
+            v = v.astype(object)
+        cols[c] = (v, t, {"inverted": c in SV_INVERTED})
+    return build_segment(name, cols)
+
+
+def random_segment(rng, n, name="seg", bits_cards=(1000, 37), raw_types=(INT, LONG, DOUBLE), inverted=(),
+                   sorted_col=False, float_col=False):
+    cols = {}
+    for i, card in enumerate(bits_cards):
+        vals = rng.integers(0, card, n) * 7 + 3  # dictionary values != dictIds
+        cols[f"d{i}"] = (vals.astype(np.int32), INT, {"inverted": f"d{i}" in inverted})
+    for t in raw_types:
+        if t == INT:
+            v = rng.integers(-1000000, 1000000, n).astype(np.int32)
+        elif t == LONG:
+            v = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+        elif t == FLOAT:
+            v = rng.normal(0, 100, n).astype(np.float32)
+        else:
+            v = rng.normal(0, 1000, n)
+        cols[f"r_{t.lower()}"] = (v, t, {"dictionary": False})
+    if sorted_col:
+        cols["ts"] = (np.sort(rng.integers(0, 50, n)).astype(np.int32), INT, {})
+    if float_col:
+        cols["fd"] = ((rng.integers(0, 20, n) * 0.25).astype(np.float64), DOUBLE, {})
+    return build_segment(name, cols)

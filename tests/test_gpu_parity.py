@@ -1,0 +1,262 @@
+"""GPU parity: the HIP path through libpinot_amd.so against the CPU oracle and the reference's
+golden values. Integer results (COUNT, SUM of integer columns, MIN/MAX, group keys, docId sets) are
+compared bit-exactly; SUM over FLOAT/DOUBLE columns within 1e-12 relative (BASELINE.json north_star)."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import SV_FILTER, load_expected, random_segment, sv_segment
+from pinot_amd import segment as S
+
+pytestmark = pytest.mark.gpu
+
+DOUBLE_SUM_RTOL = 1e-12
+EXP = load_expected()
+INNER_QUERY = "SELECT COUNT(*), SUM(column1), MAX(column3), MIN(column6), AVG(column7) FROM testTable"
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def engine(torch_cuda):
+    from pinot_amd import engine as E
+    return E
+
+
+@pytest.fixture(scope="module")
+def sv(engine):
+    bufs = sv_segment()
+    return bufs, engine.ImmutableSegment(bufs)
+
+
+def _close(a, b, float_sum=False):
+    if isinstance(a, tuple):
+        return all(_close(x, y, float_sum) for x, y in zip(a, b))
+    if float_sum and isinstance(a, float) and not (math.isinf(a) or math.isnan(a)):
+        return math.isclose(a, b, rel_tol=DOUBLE_SUM_RTOL, abs_tol=1e-300)
+    if isinstance(a, float) and math.isnan(a):
+        return isinstance(b, float) and math.isnan(b)
+    return a == b
+
+
+def assert_same_groups(got, exp, float_sum_aggs=()):
+    assert set(got) == set(exp), (sorted(set(got) ^ set(exp))[:5])
+    for k in exp:
+        for i, (g, e) in enumerate(zip(got[k], exp[k])):
+            assert _close(g, e, i in float_sum_aggs), (k, i, g, e)
+
+
+# ------------------------------------------------------------------------------- golden values
+@pytest.mark.parametrize("use_inverted", [True, False])
+@pytest.mark.parametrize("with_filter", [False, True])
+def test_golden_inner_aggregation(engine, sv, with_filter, use_inverted):
+    bufs, seg = sv
+    q = INNER_QUERY + (SV_FILTER if with_filter else "")
+    res = engine.ServerQueryExecutor(use_inverted).execute(q, [seg])
+    e = EXP["inner_aggregation"]["filter" if with_filter else "no_filter"]
+    cnt, s1, mx3, mn6, avg7 = res.groups()[()]
+    assert [cnt, s1, mx3, mn6, avg7[0], avg7[1]] == [e["count"], e["sum_column1"], e["max_column3"],
+                                                     e["min_column6"], e["avg_column7_sum"], e["avg_column7_count"]]
+    assert res.num_docs_matched() == e["count"]
+    n, og = oracle.execute(q, [bufs], use_inverted)
+    assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("case", [c for c in EXP["inner_group_by"]["cases"] if len(c["group_by"]) <= 3],
+                         ids=lambda c: f"{len(c['group_by'])}cols-f{int(c['filter'])}")
+def test_golden_inner_group_by(engine, sv, case):
+    bufs, seg = sv
+    q = INNER_QUERY + (SV_FILTER if case["filter"] else "") + " GROUP BY " + ", ".join(case["group_by"])
+    groups = engine.ServerQueryExecutor().execute(q, [seg]).groups()
+    cnt, s1, mx3, mn6, avg7 = groups[tuple(case["key"])]
+    assert [cnt, s1, mx3, mn6, avg7[0], avg7[1]] == case["values"]
+    _, og = oracle.execute(q, [bufs])
+    assert_same_groups(groups, og)
+
+
+def test_golden_inter_group_by_order_by(engine, sv):
+    bufs, seg = sv
+    for case in EXP["inter_group_by"]["cases"]:
+        q = ("SELECT " + ", ".join(case["group_by"]) + f", SUM({case['agg'][1]}) FROM testTable GROUP BY "
+             + ", ".join(case["group_by"]) + " ORDER BY " + ", ".join(case["group_by"]))
+        rows = engine.ServerQueryExecutor().execute(q, [seg] * 4).rows()
+        assert [list(r) for r in rows] == case["rows"]
+
+
+def test_golden_inter_segment(engine, sv):
+    _, seg = sv
+    ex = engine.ServerQueryExecutor()
+    for case in EXP["inter"]["cases"]:
+        names = ", ".join(f"{f}({c}) AS v{i + 1}" for i, (f, c) in enumerate(case["aggs"]))
+        q = f"SELECT {names} FROM testTable" + (SV_FILTER if case["filter"] else "")
+        if "group_by" in case:
+            order = case["order"].replace("COUNT", "v1")
+            q += f" GROUP BY {case['group_by']} ORDER BY {order} LIMIT 1"
+        rows = ex.execute(q, [seg] * 4).rows()
+        got = list(rows[0][1 if "group_by" in case else 0:])
+        for g, e in zip(got, case["result"]):
+            assert math.isclose(g, e, rel_tol=case.get("rel_tol", 0.0)), (q, got, case["result"])
+
+
+# ------------------------------------------------------------------------------- low-level operators
+@pytest.mark.parametrize("bits", [1, 2, 3, 5, 7, 8, 9, 10, 13, 16, 17, 20, 24, 27, 31])
+def test_fwd_read_dict_ids(torch_cuda, engine, bits):
+    torch = torch_cuda
+    from pinot_amd._lib import check, lib
+    rng = np.random.default_rng(bits)
+    n = 100_003
+    vals = rng.integers(0, 1 << bits, n).astype(np.int32)
+    packed = S.pack_fixed_bit(vals, bits)
+    pad = lib().pinot_amd_required_padding()
+    d = torch.zeros(len(packed) + pad, dtype=torch.uint8, device="cuda")
+    d[:len(packed)] = torch.frombuffer(bytearray(packed), dtype=torch.uint8).cuda()
+    for start, length in [(0, n), (1, 4097), (12345, 5), (n - 3, 3), (0, 0)]:
+        out = torch.full((max(length, 1),), -1, dtype=torch.int32, device="cuda")
+        check(lib().pinot_amd_fwd_read_dict_ids(d.data_ptr(), bits, start, length, out.data_ptr(), None))
+        torch.cuda.synchronize()
+        assert np.array_equal(out[:length].cpu().numpy(), vals[start:start + length])
+    # pack kernel == FixedBitSVForwardIndexWriter bytes
+    dv = torch.from_numpy(vals).cuda()
+    dp = torch.zeros(len(packed) + 8, dtype=torch.uint8, device="cuda")
+    check(lib().pinot_amd_fwd_pack_dict_ids(dv.data_ptr(), n, bits, dp.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert bytes(dp[:len(packed)].cpu().numpy()) == packed
+
+
+@pytest.mark.parametrize("t", [S.INT, S.LONG, S.FLOAT, S.DOUBLE])
+def test_fwd_read_raw(torch_cuda, t):
+    torch = torch_cuda
+    from pinot_amd._lib import check, lib
+    rng = np.random.default_rng(5)
+    npt = {S.INT: np.int32, S.LONG: np.int64, S.FLOAT: np.float32, S.DOUBLE: np.float64}[t]
+    v = (rng.normal(0, 1e9, 7777)).astype(npt)
+    raw = v.astype(v.dtype.newbyteorder(">")).tobytes()
+    d = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    out = torch.zeros(len(raw), dtype=torch.uint8, device="cuda")
+    check(lib().pinot_amd_fwd_read_raw(d.data_ptr(), {S.INT: 0, S.LONG: 1, S.FLOAT: 2, S.DOUBLE: 3}[t], 0, v.size,
+                                       out.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(npt), v)
+
+
+@pytest.mark.parametrize("num_docs", [1, 63, 64, 65, 4096, 65536, 1_000_003])
+def test_bitset_ops_and_doc_id_compaction(torch_cuda, num_docs):
+    torch = torch_cuda
+    import ctypes as C
+    from pinot_amd._lib import check, lib
+    rng = np.random.default_rng(num_docs)
+    nw = (num_docs + 63) // 64
+    a = rng.random(num_docs) < 0.3
+    b = rng.random(num_docs) < 0.6
+
+    def pack(x):
+        w = np.zeros(nw * 64, dtype=bool)
+        w[:num_docs] = x
+        return np.packbits(w.reshape(-1, 8)[:, ::-1]).view(np.uint64).copy()
+
+    da = torch.from_numpy(pack(a).view(np.int64)).cuda()
+    db = torch.from_numpy(pack(b).view(np.int64)).cuda()
+    out = torch.zeros(nw, dtype=torch.int64, device="cuda")
+    for fn, ref in (("pinot_amd_bitset_and", a & b), ("pinot_amd_bitset_or", a | b)):
+        check(getattr(lib(), fn)(da.data_ptr(), db.data_ptr(), out.data_ptr(), nw, None))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), pack(ref))
+    check(lib().pinot_amd_bitset_not(da.data_ptr(), out.data_ptr(), num_docs, None))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), pack(~a))
+    ids = torch.full((num_docs,), -1, dtype=torch.int32, device="cuda")
+    cnt = C.c_int64()
+    check(lib().pinot_amd_bitset_to_doc_ids(da.data_ptr(), num_docs, ids.data_ptr(), C.byref(cnt), None))
+    exp = np.nonzero(a)[0]
+    assert cnt.value == exp.size
+    assert np.array_equal(ids[:cnt.value].cpu().numpy(), exp)
+    c2 = C.c_int64()
+    check(lib().pinot_amd_bitset_count(db.data_ptr(), num_docs, C.byref(c2), None))
+    assert c2.value == int(b.sum())
+
+
+# ------------------------------------------------------------------------------- random sweeps vs oracle
+QUERIES = [
+    "SELECT COUNT(*), SUM(r_int), SUM(r_long), SUM(r_double), MIN(r_double), MAX(r_long) FROM t",
+    "SELECT COUNT(*), SUM(r_long) FROM t WHERE d0 BETWEEN 100 AND 4000",
+    "SELECT d1, COUNT(*), SUM(r_int), MIN(r_int), MAX(r_double), SUM(r_double) FROM t WHERE r_int > 0 GROUP BY d1",
+    "SELECT d0, d1, COUNT(*), SUM(r_long), AVG(r_int) FROM t WHERE d1 IN (3, 10, 66, 255) AND r_double < 500.5 "
+    "GROUP BY d0, d1",
+    "SELECT COUNT(*), SUM(r_int) FROM t WHERE d1 NOT IN (3, 10) OR r_long <= 0",
+    "SELECT d1, COUNT(*), MAX(d0), MIN(d0), SUM(d0) FROM t WHERE NOT (d0 > 2000 AND r_int < 5000) GROUP BY d1",
+    "SELECT COUNT(*), SUM(r_double) FROM t WHERE d0 = 31 OR d1 = 17 OR r_int = 5",
+    "SELECT COUNT(*) FROM t WHERE d0 > 999999",
+    "SELECT d1, SUM(r_double) FROM t WHERE r_double BETWEEN -10.5 AND 10.25 GROUP BY d1",
+]
+
+
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+@pytest.mark.parametrize("n", [1, 1000, 250_007])
+def test_random_queries_vs_oracle(engine, qi, n):
+    rng = np.random.default_rng(qi * 31 + n)
+    bufs = random_segment(rng, n, inverted=("d1",))
+    seg = engine.ImmutableSegment(bufs)
+    q = QUERIES[qi]
+    from pinot_amd.query import parse_sql
+    qc = parse_sql(q)
+    fsum = {i for i, a in enumerate(qc.aggregations) if a.func in ("SUM", "AVG") and a.column == "r_double"}
+    for inv in (True, False):
+        res = engine.ServerQueryExecutor(inv).execute(qc, [seg])
+        nm, og = oracle.execute(qc, [bufs], inv)
+        assert res.num_docs_matched() == nm
+        got = res.groups()
+        if not qc.group_by and nm == 0:
+            og = {(): og[()]}
+        assert_same_groups(got, og, fsum)
+
+
+def test_multi_segment_different_dictionaries(engine):
+    """Segments with different dictionaries: the combine must key on values, not dictIds."""
+    rng = np.random.default_rng(11)
+    bufs = []
+    for i in range(5):
+        n = int(rng.integers(1, 30000))
+        bufs.append(random_segment(rng, n, name=f"s{i}", bits_cards=(int(rng.integers(2, 5000)),
+                                                                     int(rng.integers(1, 300))),
+                                   sorted_col=True, float_col=True))
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    for q in ["SELECT ts, d1, COUNT(*), SUM(r_long), MIN(r_double) FROM t WHERE d0 < 5000 GROUP BY ts, d1",
+              "SELECT fd, COUNT(*), SUM(r_double), MAX(r_int) FROM t WHERE ts BETWEEN 10 AND 30 GROUP BY fd",
+              "SELECT COUNT(*), SUM(r_int) FROM t WHERE ts IN (1, 5, 9, 40) AND fd > 1.0"]:
+        res = engine.ServerQueryExecutor().execute(q, segs)
+        nm, og = oracle.execute(q, bufs)
+        assert res.num_docs_matched() == nm
+        from pinot_amd.query import parse_sql
+        qc = parse_sql(q)
+        fsum = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "r_double"}
+        assert_same_groups(res.groups(), og, fsum)
+
+
+def test_execute_again_is_idempotent(engine):
+    rng = np.random.default_rng(2)
+    bufs = random_segment(rng, 300_000)
+    seg = engine.ImmutableSegment(bufs)
+    res = engine.ServerQueryExecutor().execute(
+        "SELECT d1, COUNT(*), SUM(r_long), MAX(r_int) FROM t WHERE d0 < 3000 GROUP BY d1", [seg])
+    first = res.groups()
+    for _ in range(3):
+        res.execute_again()
+        assert res.groups() == first
+    assert res.last_kernel_ms() > 0
+
+
+def test_errors_are_loud(engine):
+    from pinot_amd._lib import PinotAmdError
+    rng = np.random.default_rng(2)
+    seg = engine.ImmutableSegment(random_segment(rng, 1000))
+    with pytest.raises(PinotAmdError):
+        engine.ServerQueryExecutor().execute("SELECT COUNT(*) FROM t WHERE nope = 1", [seg])
+    with pytest.raises(PinotAmdError):
+        engine.ServerQueryExecutor().execute("SELECT r_int, COUNT(*) FROM t GROUP BY r_int", [seg])
