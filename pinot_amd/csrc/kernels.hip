@@ -461,18 +461,23 @@ __global__ void pack_dict_ids_kernel(const int32_t* values, int64_t n, int bits,
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 8 values
   const int64_t v0 = g * 8;
   if (v0 >= n) return;
-  unsigned __int128 acc = 0;  // up to 8 * 31 = 248 bits
+  // stream the 8 values MSB-first through a 64-bit window (<= 8 + 31 live bits)
+  const int64_t total_bytes = (n * bits + 7) / 8;
+  const int64_t byte0 = g * bits;
+  const uint32_t mask = (1u << bits) - 1u;
+  uint64_t acc = 0;
+  int live = 0, ob = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const uint32_t x = v0 + k < n ? (uint32_t)values[v0 + k] : 0u;
-    acc = (acc << bits) | (unsigned __int128)(x & ((bits == 32) ? 0xFFFFFFFFu : ((1u << bits) - 1)));
-  }
-  // acc holds 8*bits bits, MSB first
-  const int nbytes = bits;  // 8 values * bits / 8
-  const int64_t byte0 = g * bits;
-  const int64_t total_bytes = (n * bits + 7) / 8;
-  for (int b = 0; b < nbytes; ++b) {
-    if (byte0 + b < total_bytes) packed[byte0 + b] = (uint8_t)(acc >> (8 * (nbytes - 1 - b)));
+    const uint32_t x = v0 + k < n ? ((uint32_t)values[v0 + k] & mask) : 0u;
+    acc = (acc << bits) | x;
+    live += bits;
+    while (live >= 8) {
+      live -= 8;
+      if (byte0 + ob < total_bytes) packed[byte0 + ob] = (uint8_t)(acc >> live);
+      ++ob;
+      acc &= (1ull << live) - 1ull;
+    }
   }
 }
 

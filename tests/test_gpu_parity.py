@@ -127,7 +127,7 @@ def test_fwd_read_dict_ids(torch_cuda, engine, bits):
     dp = torch.zeros(len(packed) + 8, dtype=torch.uint8, device="cuda")
     check(lib().pinot_amd_fwd_pack_dict_ids(dv.data_ptr(), n, bits, dp.data_ptr(), None))
     torch.cuda.synchronize()
-    assert bytes(dp[:len(packed)].cpu().numpy()) == packed
+    assert np.array_equal(dp[:len(packed)].cpu().numpy(), np.frombuffer(packed, dtype=np.uint8))
 
 
 @pytest.mark.parametrize("t", [S.INT, S.LONG, S.FLOAT, S.DOUBLE])
