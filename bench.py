@@ -38,7 +38,7 @@ def cpu_baseline(seg_rows: int, seconds: float):
     rows = 0
     t_cpu = 0.0
     k = 0
-    while t_cpu < seconds and k < 8:
+    while t_cpu < seconds and k < 64:
         bufs = datagen.ad_segment(f"cpu{k}", seg_rows, seed=10_000 + k)
         t0 = time.perf_counter()
         oracle.execute(datagen.BENCH_QUERY, [bufs])
@@ -181,7 +181,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "pamd::scan_kernel<true,false>",
+                "kernel": "pamd::scan_kernel<4,true,false>",
                 "kernel_ms": avg_kernel_s * 1e3,
                 "bytes_per_row": datagen.BENCH_BYTES_PER_ROW,
             },

@@ -22,6 +22,7 @@ namespace pamd {
 hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
                        unsigned long long* d_matched, int grid, hipStream_t st);
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st);
+int scan_blocks_per_cu(int nslots, bool lds, size_t shmem);
 hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
@@ -1134,7 +1135,8 @@ int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, in
   int dev = 0, cus = 256;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int per_cu = q.lds_keys > 0 ? std::max(1, std::min(8, (int)((160 * 1024) / std::max<int64_t>(lds_bytes, 1)))) : 8;
+  // resident blocks per CU (VGPR / LDS limited): a larger grid would only queue a second, tail-heavy wave
+  const int per_cu = scan_blocks_per_cu(q.nslots, q.lds_keys > 0, q.lds_keys > 0 ? (size_t)lds_bytes : 0);
   int64_t grid = (int64_t)cus * per_cu;
   if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
   r->grid = (int)grid;

@@ -62,29 +62,66 @@ __device__ __forceinline__ int32_t sorted_dict_id(const int32_t* starts, int32_t
   return lo;
 }
 
-// Decoded per-slot representation: dictIds (dict columns), INT/LONG values, or FLOAT/DOUBLE as
-// double bits.
-__device__ __forceinline__ void load_slot(const DevColumn& c, int64_t doc0, int64_t v[4]) {
+// A lane's raw words for one column of one tile: fetched early (prefetch), decoded later.
+struct Raw {
+  uint4 a, b;
+};
+
+// Issue the loads of a column's 4 docs at doc0: fixed-bit = 5-dword window, raw 4 B = one 16 B
+// load, raw 8 B = two 16 B loads. Sorted columns are decoded by dependent lookups (no fetch).
+// Every path assigns both vectors whole so the words stay in registers.
+__device__ __forceinline__ Raw fetch_slot(const DevColumn& c, int64_t doc0) {
+  Raw r;
   if (c.enc == ENC_FIXED_BIT) {
-    load_fixed_bit4(c.data, c.bits, doc0, v);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(c.data) + ((doc0 * c.bits) >> 5);
+    r.a = make_uint4(w[0], w[1], w[2], w[3]);
+    r.b = make_uint4(w[4], 0u, 0u, 0u);
   } else if (c.enc == ENC_RAW) {
     if (c.type == T_INT || c.type == T_FLOAT) {
-      const uint4 q = *reinterpret_cast<const uint4*>(c.data + doc0 * 4);
-      const uint32_t e[4] = {bswap32(q.x), bswap32(q.y), bswap32(q.z), bswap32(q.w)};
-      if (c.type == T_INT) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (int64_t)(int32_t)e[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = __double_as_longlong((double)__uint_as_float(e[k]));
-      }
+      r.a = *reinterpret_cast<const uint4*>(c.data + doc0 * 4);
+      r.b = make_uint4(0u, 0u, 0u, 0u);
     } else {
-      const uint4 a = *reinterpret_cast<const uint4*>(c.data + doc0 * 8);
-      const uint4 b = *reinterpret_cast<const uint4*>(c.data + doc0 * 8 + 16);
-      v[0] = (int64_t)bswap64(a.x, a.y);
-      v[1] = (int64_t)bswap64(a.z, a.w);
-      v[2] = (int64_t)bswap64(b.x, b.y);
-      v[3] = (int64_t)bswap64(b.z, b.w);
+      r.a = *reinterpret_cast<const uint4*>(c.data + doc0 * 8);
+      r.b = *reinterpret_cast<const uint4*>(c.data + doc0 * 8 + 16);
+    }
+  } else {
+    r.a = make_uint4(0u, 0u, 0u, 0u);
+    r.b = r.a;
+  }
+  return r;
+}
+
+// Decoded per-slot representation: dictIds (dict columns), INT/LONG values, or FLOAT/DOUBLE as
+// double bits.
+__device__ __forceinline__ void decode_slot(const DevColumn& c, int64_t doc0, const Raw& r, int64_t v[4]) {
+  if (c.enc == ENC_FIXED_BIT) {
+    const int bits = c.bits;
+    const uint32_t rr = (uint32_t)((doc0 * bits) & 31);
+    const uint32_t x0 = bswap32(r.a.x), x1 = bswap32(r.a.y), x2 = bswap32(r.a.z), x3 = bswap32(r.a.w),
+                   x4 = bswap32(r.b.x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t p = rr + (uint32_t)(k * bits);
+      const uint32_t i = p >> 5, sh = p & 31;
+      const uint64_t win = ((uint64_t)sel4(i, x0, x1, x2, x3) << 32) | sel4(i, x1, x2, x3, x4);
+      v[k] = (int64_t)((win << sh) >> (64 - bits));
+    }
+  } else if (c.enc == ENC_RAW) {
+    if (c.type == T_INT) {
+      v[0] = (int64_t)(int32_t)bswap32(r.a.x);
+      v[1] = (int64_t)(int32_t)bswap32(r.a.y);
+      v[2] = (int64_t)(int32_t)bswap32(r.a.z);
+      v[3] = (int64_t)(int32_t)bswap32(r.a.w);
+    } else if (c.type == T_FLOAT) {
+      v[0] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.x)));
+      v[1] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.y)));
+      v[2] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.z)));
+      v[3] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.w)));
+    } else {
+      v[0] = (int64_t)bswap64(r.a.x, r.a.y);
+      v[1] = (int64_t)bswap64(r.a.z, r.a.w);
+      v[2] = (int64_t)bswap64(r.b.x, r.b.y);
+      v[3] = (int64_t)bswap64(r.b.z, r.b.w);
     }
   } else {  // ENC_SORTED
     const int32_t* starts = reinterpret_cast<const int32_t*>(c.data);
@@ -240,7 +277,7 @@ __device__ __forceinline__ uint64_t acc_identity(int32_t op) {
 //   kBitset: also write the filter's docId bitset (per segment, at bitset_out[s] words)
 //   kLds:    accumulate into an LDS-privatised table of q.lds_keys keys, flushed once per block
 // ------------------------------------------------------------------------------------------------
-template <bool kLds, bool kBitset>
+template <int NS, bool kLds, bool kBitset>
 __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restrict__ segs, const DevQuery q,
                                                       uint64_t* __restrict__ acc,      // [nacc][num_keys]
                                                       uint64_t* const* __restrict__ bitset_out,
@@ -274,25 +311,47 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
     s = lo;
   }
 
+  auto doc_of = [&](int seg_idx, int64_t t) -> int64_t {
+    return (t - segs[seg_idx].tile_begin) * kTileDocs + (int64_t)tid * kDocsPerThread;
+  };
+  // software pipeline: the next tile's column words are in flight while this tile is processed
+  Raw rc[NS];
+#pragma unroll
+  for (int sl = 0; sl < NS; ++sl) {
+    rc[sl].a = make_uint4(0u, 0u, 0u, 0u);
+    rc[sl].b = rc[sl].a;
+    if (t_begin < t_end && sl < q.nslots) rc[sl] = fetch_slot(segs[s].cols[sl], doc_of(s, t_begin));
+  }
+
   for (int64_t t = t_begin; t < t_end; ++t) {
-    while (s + 1 < q.nsegs && segs[s + 1].tile_begin <= t) ++s;
     const DevSegment& seg = segs[s];
-    const int64_t doc0 = (t - seg.tile_begin) * kTileDocs + (int64_t)tid * kDocsPerThread;
+    const int64_t doc0 = doc_of(s, t);
     const int64_t nd = seg.num_docs;
     uint32_t match = doc0 + 4 <= nd ? 0xFu : doc0 >= nd ? 0u : (0xFu >> (4 - (nd - doc0)));
 
-    // ---- decode every referenced column (compile-time slot indices only) ----
-    int64_t v[kMaxSlots][4];
+    int s_next = s;
+    while (s_next + 1 < q.nsegs && segs[s_next + 1].tile_begin <= t + 1) ++s_next;
+    Raw rn[NS];
+    const int64_t doc_n = doc_of(s_next, t + 1);
 #pragma unroll
-    for (int sl = 0; sl < kMaxSlots; ++sl) {
-      if (sl < q.nslots) load_slot(seg.cols[sl], doc0, v[sl]);
+    for (int sl = 0; sl < NS; ++sl) {
+      rn[sl].a = make_uint4(0u, 0u, 0u, 0u);
+      rn[sl].b = rn[sl].a;
+      if (t + 1 < t_end && sl < q.nslots) rn[sl] = fetch_slot(segs[s_next].cols[sl], doc_n);
+    }
+
+    // ---- decode every referenced column (compile-time slot indices only) ----
+    int64_t v[NS][4];
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+      if (sl < q.nslots) decode_slot(seg.cols[sl], doc0, rc[sl], v[sl]);
     }
 
     // ---- filter: AND over clauses of OR over leaves ----
     if (q.nleaves > 0) {
       uint64_t clause_bits = 0;
 #pragma unroll
-      for (int sl = 0; sl < kMaxSlots; ++sl) {
+      for (int sl = 0; sl < NS; ++sl) {
         if (sl < q.nslots) {
           for (int l = q.slot_leaf_begin[sl]; l < q.slot_leaf_begin[sl + 1]; ++l) {
             const DevLeaf& L = seg.leaves[l];
@@ -316,12 +375,13 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
     }
 
     matched += __builtin_popcount(match);
-    if (q.nacc == 0) continue;
+    do {  // aggregation; `break` leaves it, the pipeline rotation below always runs
+    if (q.nacc == 0) break;
 
     // ---- group key per doc ----
     int64_t key[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int sl = 0; sl < kMaxSlots; ++sl) {
+    for (int sl = 0; sl < NS; ++sl) {
       if (sl < q.nslots && q.slot_group_stride[sl] > 0) {
         const int32_t* remap = seg.cols[sl].remap;
         const int64_t st = q.slot_group_stride[sl];
@@ -340,7 +400,7 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
 #pragma unroll
     for (int k = 0; k < 4; ++k) lane_uniform &= !((match >> k) & 1) || key[k] == kA;
     const unsigned long long has_mask = __ballot(lane_has);
-    if (has_mask == 0) continue;
+    if (has_mask == 0) break;
     const int src = __ffsll((long long)has_mask) - 1;
     const int64_t kW = __shfl(kA, src, 64);
     const bool wave_uniform = __ballot(lane_has && (!lane_uniform || kA != kW)) == 0;
@@ -350,7 +410,7 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
       const int64_t cnt = wave_sum_i64(__builtin_popcount(match));
       if (lane == 0) acc_apply(ACC_COUNT, row, (uint64_t)cnt);
 #pragma unroll
-      for (int sl = 0; sl < kMaxSlots; ++sl) {
+      for (int sl = 0; sl < NS; ++sl) {
         if (sl < q.nslots) {
           const DevColumn& col = seg.cols[sl];
           for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
@@ -396,7 +456,7 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
           uint64_t* row = table + key[k];
           acc_apply(ACC_COUNT, row, 1);
 #pragma unroll
-          for (int sl = 0; sl < kMaxSlots; ++sl) {
+          for (int sl = 0; sl < NS; ++sl) {
             if (sl < q.nslots) {
               const DevColumn& col = seg.cols[sl];
               for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
@@ -416,6 +476,11 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
         }
       }
     }
+    } while (0);
+
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) rc[sl] = rn[sl];
+    s = s_next;
   }
 
   // ---- per-block results ----
@@ -636,26 +701,49 @@ static inline unsigned grid_for(int64_t n, int per_block) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
+template <int NS>
+static hipError_t launch_scan_ns(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc,
+                                 unsigned long long* d_matched, int grid, size_t shmem, hipStream_t st) {
+  if (q.lds_keys > 0)
+    hipLaunchKernelGGL((scan_kernel<NS, true, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, nullptr,
+                       d_matched);
+  else
+    hipLaunchKernelGGL((scan_kernel<NS, false, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
+                       nullptr, d_matched);
+  return hipGetLastError();
+}
+
+// slot-count variant: decoded values live in NS x 4 registers, so a 4-column query does not pay
+// the register cost (and occupancy) of the 8-column kernel
+static inline int ns_for(int nslots) { return nslots <= 1 ? 1 : nslots <= 2 ? 2 : nslots <= 4 ? 4 : 8; }
+
 hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
                        unsigned long long* d_matched, int grid, hipStream_t st) {
-  const bool lds = q.lds_keys > 0;
-  const size_t shmem = lds ? (size_t)q.nacc * q.lds_keys * 8 : 0;
-  if (d_bitsets) {
-    if (lds)
-      hipLaunchKernelGGL((scan_kernel<true, true>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, d_bitsets,
-                         d_matched);
-    else
-      hipLaunchKernelGGL((scan_kernel<false, true>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
-                         d_bitsets, d_matched);
-  } else {
-    if (lds)
-      hipLaunchKernelGGL((scan_kernel<true, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, nullptr,
-                         d_matched);
-    else
-      hipLaunchKernelGGL((scan_kernel<false, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
-                         nullptr, d_matched);
+  const size_t shmem = q.lds_keys > 0 ? (size_t)q.nacc * q.lds_keys * 8 : 0;
+  if (d_bitsets) return hipErrorNotSupported;
+  switch (ns_for(q.nslots)) {
+    case 1: return launch_scan_ns<1>(d_segs, q, d_acc, d_matched, grid, shmem, st);
+    case 2: return launch_scan_ns<2>(d_segs, q, d_acc, d_matched, grid, shmem, st);
+    case 4: return launch_scan_ns<4>(d_segs, q, d_acc, d_matched, grid, shmem, st);
+    default: return launch_scan_ns<8>(d_segs, q, d_acc, d_matched, grid, shmem, st);
   }
-  return hipGetLastError();
+}
+
+template <int NS>
+static int occupancy_ns(bool lds, size_t shmem) {
+  int n = 0;
+  const hipError_t e = lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<NS, true, false>, kBlock, shmem)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<NS, false, false>, kBlock, shmem);
+  return (e == hipSuccess && n > 0) ? n : 1;
+}
+
+int scan_blocks_per_cu(int nslots, bool lds, size_t shmem) {
+  switch (ns_for(nslots)) {
+    case 1: return occupancy_ns<1>(lds, shmem);
+    case 2: return occupancy_ns<2>(lds, shmem);
+    case 4: return occupancy_ns<4>(lds, shmem);
+    default: return occupancy_ns<8>(lds, shmem);
+  }
 }
 
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st) {
