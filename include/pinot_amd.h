@@ -183,6 +183,14 @@ typedef struct pinot_amd_result pinot_amd_result;
  * fetched. The group key space across segments is the union of their dictionaries. */
 int pinot_amd_execute(pinot_amd_query* q, pinot_amd_segment* const* segs, int32_t n, void* stream,
                       pinot_amd_result** out);
+/* FilterPlanNode -> BlockDocIdSet for each segment: evaluates only q's filter and keeps, per segment,
+ * a dense docId bitset in HBM (bit d of word d/64 set <=> doc d matches), readable with
+ * pinot_amd_result_bitset and convertible to ascending docIds with pinot_amd_bitset_to_doc_ids. */
+int pinot_amd_execute_filter(pinot_amd_query* q, pinot_amd_segment* const* segs, int32_t n, void* stream,
+                             pinot_amd_result** out);
+/* Device pointer and word count of segment `segment_index`'s docId bitset of a filter-only result. */
+int pinot_amd_result_bitset(pinot_amd_result* r, int32_t segment_index, const uint64_t** h_d_bitset,
+                            int64_t* h_num_words);
 /* Re-run a query whose plan was compiled by pinot_amd_execute on the same segments (no host work
  * beyond the launches): the benchmarked step. */
 int pinot_amd_execute_again(pinot_amd_result* r, void* stream);

@@ -598,6 +598,9 @@ struct pinot_amd_result {
   };
   std::vector<InvLeaf> inv_leaves;
   int grid = 1;
+  std::vector<std::unique_ptr<DevBuf>> bitsets;  // filter-only plans: one docId bitset per segment
+  std::vector<int64_t> bitset_words;
+  DevBuf d_bitset_ptrs;
   DevBuf acc;
   DevBuf matched;
   std::vector<MergedKeyColumn> keys;  // merged dictionaries of the group-by columns
@@ -906,7 +909,8 @@ static int run_plan(pinot_amd_result* r) {
   HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
   if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
   HIP_OK(hipEventRecord(r->ev0, st));
-  HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p, nullptr,
+  HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p,
+                     r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p,
                      (unsigned long long*)r->matched.p, r->grid, st));
   HIP_OK(hipEventRecord(r->ev1, st));
   return 0;
@@ -914,14 +918,16 @@ static int run_plan(pinot_amd_result* r) {
 
 extern "C" {
 
-int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
-                      pinot_amd_result** out) {
+static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
+                        bool filter_only, pinot_amd_result** out) {
   if (!qq || !segs_in || n < 1 || !out) return fail(PINOT_AMD_EINVAL, "execute: bad arguments");
   std::vector<pinot_amd_segment*> segs(segs_in, segs_in + n);
   auto res = std::make_unique<pinot_amd_result>();
   pinot_amd_result* r = res.get();
   r->stream = (hipStream_t)stream;
-  const pinot_amd_query& Q = *qq;
+  pinot_amd_query filter_q;
+  if (filter_only) filter_q.preds = qq->preds;  // FilterPlanNode only: no projection, no aggregation
+  const pinot_amd_query& Q = filter_only ? filter_q : *qq;
 
   // ---- slots: columns the kernel must decode ----
   std::vector<std::string> slot_cols;
@@ -1126,6 +1132,21 @@ int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, in
 
   int rc = r->d_segs.alloc_copy(r->hsegs.data(), r->hsegs.size() * sizeof(DevSegment), 0);
   if (rc) return rc;
+  if (filter_only) {
+    std::vector<uint64_t*> ptrs;
+    for (int si = 0; si < n; ++si) {
+      const int64_t words = std::max<int64_t>((segs[si]->num_docs + kTileDocs - 1) / kTileDocs, 1) * (kTileDocs / 64);
+      auto b = std::make_unique<DevBuf>();
+      rc = b->alloc((size_t)words * 8);
+      if (rc) return rc;
+      HIP_OK(hipMemset(b->p, 0, b->n));
+      ptrs.push_back((uint64_t*)b->p);
+      r->bitset_words.push_back(words);
+      r->bitsets.push_back(std::move(b));
+    }
+    rc = r->d_bitset_ptrs.alloc_copy(ptrs.data(), ptrs.size() * sizeof(uint64_t*), 0);
+    if (rc) return rc;
+  }
   rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * num_keys * 8);
   if (rc) return rc;
   rc = r->matched.alloc(8);
@@ -1145,6 +1166,28 @@ int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, in
   rc = run_plan(r);
   if (rc) return rc;
   *out = res.release();
+  return 0;
+}
+
+int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
+                      pinot_amd_result** out) {
+  return execute_impl(qq, segs_in, n, stream, false, out);
+}
+
+int pinot_amd_execute_filter(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
+                             pinot_amd_result** out) {
+  return execute_impl(qq, segs_in, n, stream, true, out);
+}
+
+int pinot_amd_result_bitset(pinot_amd_result* r, int32_t segment_index, const uint64_t** h_d_bitset,
+                            int64_t* h_num_words) {
+  if (!r || !h_d_bitset || !h_num_words) return fail(PINOT_AMD_EINVAL, "result_bitset: bad arguments");
+  if (r->bitsets.empty()) return fail(PINOT_AMD_EINVAL, "result_bitset: not a filter-only result");
+  if (segment_index < 0 || segment_index >= (int32_t)r->bitsets.size())
+    return fail(PINOT_AMD_EINVAL, "result_bitset: segment index %d out of range", segment_index);
+  HIP_OK(hipStreamSynchronize(r->stream));
+  *h_d_bitset = (const uint64_t*)r->bitsets[segment_index]->p;
+  *h_num_words = r->bitset_words[segment_index];
   return 0;
 }
 

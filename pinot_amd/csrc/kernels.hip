@@ -703,8 +703,12 @@ static inline unsigned grid_for(int64_t n, int per_block) {
 
 template <int NS>
 static hipError_t launch_scan_ns(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc,
-                                 unsigned long long* d_matched, int grid, size_t shmem, hipStream_t st) {
-  if (q.lds_keys > 0)
+                                 uint64_t* const* d_bitsets, unsigned long long* d_matched, int grid, size_t shmem,
+                                 hipStream_t st) {
+  if (d_bitsets)  // filter-only plan (FilterPlanNode -> docId set): no accumulators
+    hipLaunchKernelGGL((scan_kernel<NS, false, true>), dim3(grid), dim3(kBlock), 0, st, d_segs, q, d_acc, d_bitsets,
+                       d_matched);
+  else if (q.lds_keys > 0)
     hipLaunchKernelGGL((scan_kernel<NS, true, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, nullptr,
                        d_matched);
   else
@@ -720,12 +724,12 @@ static inline int ns_for(int nslots) { return nslots <= 1 ? 1 : nslots <= 2 ? 2 
 hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
                        unsigned long long* d_matched, int grid, hipStream_t st) {
   const size_t shmem = q.lds_keys > 0 ? (size_t)q.nacc * q.lds_keys * 8 : 0;
-  if (d_bitsets) return hipErrorNotSupported;
+  if (d_bitsets && q.nacc > 0) return hipErrorNotSupported;
   switch (ns_for(q.nslots)) {
-    case 1: return launch_scan_ns<1>(d_segs, q, d_acc, d_matched, grid, shmem, st);
-    case 2: return launch_scan_ns<2>(d_segs, q, d_acc, d_matched, grid, shmem, st);
-    case 4: return launch_scan_ns<4>(d_segs, q, d_acc, d_matched, grid, shmem, st);
-    default: return launch_scan_ns<8>(d_segs, q, d_acc, d_matched, grid, shmem, st);
+    case 1: return launch_scan_ns<1>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
+    case 2: return launch_scan_ns<2>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
+    case 4: return launch_scan_ns<4>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
+    default: return launch_scan_ns<8>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
   }
 }
 

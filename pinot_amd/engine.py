@@ -247,6 +247,54 @@ class ServerQueryExecutor:
     def __init__(self, use_inverted_index: bool = True):
         self.use_inverted_index = use_inverted_index
 
+    def filter_doc_ids(self, query, segments: Sequence[ImmutableSegment], stream=None) -> List[np.ndarray]:
+        """FilterPlanNode -> BlockDocIdSet: ascending matching docIds of each segment (the filter
+        runs on the device into a dense bitset, compacted with ballot / prefix sums)."""
+        import torch
+        qc = parse_sql(query) if isinstance(query, str) else query
+        L = lib()
+        qh = self._compile(qc, segments)
+        try:
+            arr = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
+            rh = C.c_void_p()
+            check(L.pinot_amd_execute_filter(qh, arr, len(segments), _stream_handle(stream), C.byref(rh)),
+                  "execute_filter")
+        finally:
+            L.pinot_amd_query_destroy(qh)
+        out = []
+        try:
+            for i, seg in enumerate(segments):
+                p = C.c_void_p()
+                nw = C.c_int64()
+                check(L.pinot_amd_result_bitset(rh, i, C.byref(p), C.byref(nw)), "result_bitset")
+                ids = torch.empty(max(seg.num_docs, 1), dtype=torch.int32, device="cuda")
+                cnt = C.c_int64()
+                check(L.pinot_amd_bitset_to_doc_ids(p.value, seg.num_docs, ids.data_ptr(), C.byref(cnt),
+                                                    _stream_handle(stream)), "bitset_to_doc_ids")
+                out.append(ids[:cnt.value].cpu().numpy())
+        finally:
+            L.pinot_amd_result_destroy(rh)
+        return out
+
+    def _compile(self, qc: QueryContext, segments: Sequence[ImmutableSegment]):
+        L = lib()
+        first = segments[0]
+        qh = C.c_void_p()
+        check(L.pinot_amd_query_create(C.byref(qh)), "query_create")
+        keep: list = []
+        try:
+            for ci, clause in enumerate(qc.cnf):
+                for pred, neg in clause:
+                    col = first.columns.get(pred.column)
+                    if col is None:
+                        raise _lib.PinotAmdError(f"unknown column {pred.column!r} in segment {first.name}")
+                    spec = _predicate_spec(pred, col, self.use_inverted_index, keep)
+                    check(L.pinot_amd_query_add_predicate(qh, ci, C.byref(spec), 1 if neg else 0), "add_predicate")
+        except Exception:
+            L.pinot_amd_query_destroy(qh)
+            raise
+        return qh
+
     def execute(self, query, segments: Sequence[ImmutableSegment], stream=None) -> QueryResult:
         qc = parse_sql(query) if isinstance(query, str) else query
         if not segments:

@@ -260,3 +260,44 @@ def test_errors_are_loud(engine):
         engine.ServerQueryExecutor().execute("SELECT COUNT(*) FROM t WHERE nope = 1", [seg])
     with pytest.raises(PinotAmdError):
         engine.ServerQueryExecutor().execute("SELECT r_int, COUNT(*) FROM t GROUP BY r_int", [seg])
+
+
+FILTERS = [
+    " WHERE d0 BETWEEN 100 AND 4000",
+    " WHERE d1 IN (3, 10, 66, 255) AND r_double < 500.5",
+    " WHERE d1 NOT IN (3, 10) OR r_long <= 0",
+    " WHERE NOT (d0 > 2000 AND r_int < 5000)",
+    " WHERE r_int = 5 OR d0 = 31",
+    " WHERE d0 > 999999",
+]
+
+
+@pytest.mark.parametrize("fi", range(len(FILTERS)))
+@pytest.mark.parametrize("n", [1, 1023, 1025, 200_003])
+def test_filter_doc_id_sets(engine, fi, n):
+    """FilterPlanNode -> docId set: bit-exact docIds (ascending) against the oracle's filter."""
+    rng = np.random.default_rng(fi * 7 + n)
+    bufs = random_segment(rng, n, inverted=("d1",))
+    seg = engine.ImmutableSegment(bufs)
+    q = "SELECT COUNT(*) FROM t" + FILTERS[fi]
+    for inv in (True, False):
+        got = engine.ServerQueryExecutor(inv).filter_doc_ids(q, [seg, seg])
+        bits, cnt = oracle.OracleSegment(bufs).filter_bitset(__import__("pinot_amd.query").query.parse_sql(q), inv)
+        ids = np.zeros(max(n, 1), dtype=np.int32)
+        m = oracle.lib().oracle_bitset_to_doc_ids(bits.ctypes.data, n, ids.ctypes.data)
+        assert m == cnt
+        for g in got:
+            assert np.array_equal(g, ids[:m])
+
+
+def test_golden_filter_doc_ids(engine, sv):
+    """The reference FILTER over the golden segment selects 6129 docs; docIds match the oracle."""
+    bufs, seg = sv
+    from pinot_amd.query import parse_sql
+    q = "SELECT COUNT(*) FROM testTable" + SV_FILTER
+    (got,) = engine.ServerQueryExecutor().filter_doc_ids(q, [seg])
+    assert got.size == EXP["inner_aggregation"]["filter"]["count"]
+    bits, cnt = oracle.OracleSegment(bufs).filter_bitset(parse_sql(q))
+    ids = np.zeros(bufs.num_docs, dtype=np.int32)
+    m = oracle.lib().oracle_bitset_to_doc_ids(bits.ctypes.data, bufs.num_docs, ids.ctypes.data)
+    assert np.array_equal(got, ids[:m])
