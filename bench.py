@@ -173,6 +173,7 @@ def main():
                 "parallelism": f"segments sharded over {world} GPU(s), RCCL all-reduce merge" if world > 1
                                else "1 GPU",
                 "hbm_bytes_per_gpu": hbm,
+                "scan_kernel": res.kernel_info(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -181,7 +182,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "pamd::scan_kernel<4,true,false>",
+                "kernel": "pinot_scan_jit" if res.kernel_info() == "jit" else "pamd::scan_kernel<4,true,false>",
                 "kernel_ms": avg_kernel_s * 1e3,
                 "bytes_per_row": datagen.BENCH_BYTES_PER_ROW,
             },

@@ -65,6 +65,9 @@ int pinot_amd_abi_version(void);
 const char* pinot_amd_last_error(void);
 /* hipSetDevice for the calling thread; one process drives one GPU. */
 int pinot_amd_set_device(int device);
+/* Diagnostic: generate and hipRTC-compile a spread of query-specialised scan kernels (no device
+ * needed). Returns 0 when every shape compiles; verbose != 0 prints each shape (and failures). */
+int pinot_amd_jit_selftest(int verbose);
 /* Bytes of slack the kernels may read past the end of a column buffer handed to the
  * low-level entry points (segments staged by pinot_amd_segment_* are padded internally). */
 size_t pinot_amd_required_padding(void);
@@ -213,6 +216,9 @@ const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t 
  * 1 = sum(double), 2 = min(uint64 ordered), 3 = max(uint64 ordered). */
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops);
+/* Which scan kernel the plan runs: "jit" (query-specialised, compiled with hipRTC) or
+ * "aot: <reason>" (the generic precompiled kernel). */
+const char* pinot_amd_result_kernel_info(pinot_amd_result* r);
 /* Kernel timing of the last execute: device milliseconds of the fused scan kernel, measured with
  * HIP events on the execution stream. */
 int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms);

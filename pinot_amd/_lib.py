@@ -56,6 +56,7 @@ SIGNATURES = {
     "pinot_amd_last_error": (C.c_char_p, []),
     "pinot_amd_set_device": (C.c_int, [C.c_int]),
     "pinot_amd_required_padding": (C.c_size_t, []),
+    "pinot_amd_jit_selftest": (C.c_int, [C.c_int]),
     "pinot_amd_segment_create": (C.c_int, [C.c_char_p, C.c_int64, _PP]),
     "pinot_amd_segment_add_column": (C.c_int, [_P, C.POINTER(ColumnSpec)]),
     "pinot_amd_segment_destroy": (C.c_int, [_P]),
@@ -87,6 +88,7 @@ SIGNATURES = {
     "pinot_amd_result_string_key": (C.c_char_p, [_P, C.c_int32, C.c_int64]),
     "pinot_amd_result_accumulators": (C.c_int, [_P, C.POINTER(C.c_int32), _I64P, _PP, C.POINTER(C.c_int32)]),
     "pinot_amd_result_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "pinot_amd_result_kernel_info": (C.c_char_p, [_P]),
 }
 
 _lib = None

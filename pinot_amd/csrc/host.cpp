@@ -17,6 +17,7 @@
 
 #include "../../include/pinot_amd.h"
 #include "device_types.h"
+#include "jit.h"
 
 namespace pamd {
 hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
@@ -610,6 +611,9 @@ struct pinot_amd_result {
   int32_t num_group_by = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
+  JitKernel* jit = nullptr;      // query-specialised kernel (nullptr: AOT scan_kernel)
+  std::string jit_status;        // why the AOT kernel runs, if it does
+  size_t shmem = 0;
   ~pinot_amd_result() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -909,9 +913,19 @@ static int run_plan(pinot_amd_result* r) {
   HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
   if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
   HIP_OK(hipEventRecord(r->ev0, st));
-  HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p,
-                     r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p,
-                     (unsigned long long*)r->matched.p, r->grid, st));
+  if (r->jit) {
+    const DevSegment* segs = (const DevSegment*)r->d_segs.p;
+    uint64_t* acc = (uint64_t*)r->acc.p;
+    uint64_t* const* bits = r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p;
+    unsigned long long* matched = (unsigned long long*)r->matched.p;
+    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched};
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem, st, args,
+                                 nullptr));
+  } else {
+    HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p,
+                       r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p,
+                       (unsigned long long*)r->matched.p, r->grid, st));
+  }
   HIP_OK(hipEventRecord(r->ev1, st));
   return 0;
 }
@@ -1152,12 +1166,60 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   rc = r->matched.alloc(8);
   if (rc) return rc;
 
+  // query-specialised kernel (hipRTC): needs every slot's encoding to agree across the batch
+  {
+    JitPlan jp;
+    bool ok = true;
+    for (int sl = 0; sl < nslots && ok; ++sl) {
+      const int enc = r->hsegs[0].cols[sl].enc;
+      for (int si = 1; si < n; ++si) ok &= r->hsegs[si].cols[sl].enc == enc;
+      jp.slots.push_back({enc, r->hsegs[0].cols[sl].type});
+    }
+    for (size_t k = 0; k < order.size(); ++k) {
+      JitLeaf jl{pred_slot[order[k]], Q.preds[order[k]].clause, r->hsegs[0].leaves[k].negate, 0u};
+      for (int si = 0; si < n; ++si) {
+        ok &= r->hsegs[si].leaves[k].negate == jl.negate;
+        jl.kinds |= 1u << r->hsegs[si].leaves[k].kind;
+      }
+      jp.leaves.push_back(jl);
+    }
+    jp.nclauses = nclauses;
+    for (size_t j = 0; j < Q.group_by.size(); ++j) {
+      const int sl = slot_of(Q.group_by[j]);
+      jp.group.push_back({sl, r->key_stride[j]});
+      for (int si = 0; si < n; ++si) jp.any_remap |= r->hsegs[si].cols[sl].remap != nullptr;
+    }
+    for (int a = 1; a < q.nacc; ++a) {
+      int sl = 0;
+      while (sl < kMaxSlots && !(a >= q.slot_acc_begin[sl] && a < q.slot_acc_begin[sl + 1])) ++sl;
+      jp.accs.push_back({q.acc_op[a], sl});
+    }
+    jp.num_keys = num_keys;
+    jp.lds = q.lds_keys > 0;
+    jp.bitset = filter_only;
+    jp.aggregate = q.nacc > 0;
+    if (ok) {
+      r->jit = jit_get(jp, &r->jit_status);
+    } else {
+      r->jit_status = "segments disagree on a column's encoding";
+    }
+  }
+  r->shmem = q.lds_keys > 0 ? (size_t)lds_bytes : 0;
+
   // persistent grid: enough blocks to fill every CU at the occupancy the LDS table allows
   int dev = 0, cus = 256;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   // resident blocks per CU (VGPR / LDS limited): a larger grid would only queue a second, tail-heavy wave
-  const int per_cu = scan_blocks_per_cu(q.nslots, q.lds_keys > 0, q.lds_keys > 0 ? (size_t)lds_bytes : 0);
+  int per_cu = 1;
+  if (r->jit) {
+    int nb = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock, r->shmem) != hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = nb;
+  } else {
+    per_cu = scan_blocks_per_cu(q.nslots, q.lds_keys > 0, r->shmem);
+  }
   int64_t grid = (int64_t)cus * per_cu;
   if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
   r->grid = (int)grid;
@@ -1207,6 +1269,13 @@ int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   HIP_OK(hipMemcpyAsync(h_out, r->matched.p, 8, hipMemcpyDeviceToHost, r->stream));
   HIP_OK(hipStreamSynchronize(r->stream));
   return 0;
+}
+
+const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
+  if (!r) return "";
+  static thread_local std::string info;
+  info = r->jit ? "jit" : ("aot: " + r->jit_status);
+  return info.c_str();
 }
 
 int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms) {

@@ -171,6 +171,10 @@ class QueryResult:
         check(lib().pinot_amd_result_num_docs_matched(self._h, C.byref(out)), "num_docs_matched")
         return out.value
 
+    def kernel_info(self) -> str:
+        """'jit' when the query-specialised kernel runs, else 'aot: <reason>'."""
+        return lib().pinot_amd_result_kernel_info(self._h).decode()
+
     def last_kernel_ms(self) -> float:
         out = C.c_double()
         check(lib().pinot_amd_result_last_kernel_ms(self._h, C.byref(out)), "last_kernel_ms")

@@ -140,3 +140,9 @@ def test_capi_exports_every_declared_symbol():
         assert hasattr(L, name), name
     assert L.pinot_amd_abi_version() == 1
     assert L.pinot_amd_required_padding() >= 8192
+
+
+def test_jit_codegen_compiles_for_gfx950():
+    """The query-specialised kernels the planner generates compile with hipRTC (no device needed)."""
+    from pinot_amd import _lib
+    assert _lib.lib().pinot_amd_jit_selftest(0) == 0

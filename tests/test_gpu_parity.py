@@ -30,6 +30,18 @@ def engine(torch_cuda):
     return E
 
 
+@pytest.fixture(params=["jit", "aot"])
+def kernel_mode(request, monkeypatch):
+    """Run a test through the hipRTC query-specialised kernel and through the AOT generic kernel."""
+    monkeypatch.setenv("PINOT_AMD_JIT", "1" if request.param == "jit" else "0")
+    return request.param
+
+
+def check_mode(res, mode):
+    info = res.kernel_info()
+    assert info.startswith(mode), info
+
+
 @pytest.fixture(scope="module")
 def sv(engine):
     bufs = sv_segment()
@@ -56,10 +68,11 @@ def assert_same_groups(got, exp, float_sum_aggs=()):
 # ------------------------------------------------------------------------------- golden values
 @pytest.mark.parametrize("use_inverted", [True, False])
 @pytest.mark.parametrize("with_filter", [False, True])
-def test_golden_inner_aggregation(engine, sv, with_filter, use_inverted):
+def test_golden_inner_aggregation(engine, sv, with_filter, use_inverted, kernel_mode):
     bufs, seg = sv
     q = INNER_QUERY + (SV_FILTER if with_filter else "")
     res = engine.ServerQueryExecutor(use_inverted).execute(q, [seg])
+    check_mode(res, kernel_mode)
     e = EXP["inner_aggregation"]["filter" if with_filter else "no_filter"]
     cnt, s1, mx3, mn6, avg7 = res.groups()[()]
     assert [cnt, s1, mx3, mn6, avg7[0], avg7[1]] == [e["count"], e["sum_column1"], e["max_column3"],
@@ -71,17 +84,19 @@ def test_golden_inner_aggregation(engine, sv, with_filter, use_inverted):
 
 @pytest.mark.parametrize("case", [c for c in EXP["inner_group_by"]["cases"] if len(c["group_by"]) <= 3],
                          ids=lambda c: f"{len(c['group_by'])}cols-f{int(c['filter'])}")
-def test_golden_inner_group_by(engine, sv, case):
+def test_golden_inner_group_by(engine, sv, case, kernel_mode):
     bufs, seg = sv
     q = INNER_QUERY + (SV_FILTER if case["filter"] else "") + " GROUP BY " + ", ".join(case["group_by"])
-    groups = engine.ServerQueryExecutor().execute(q, [seg]).groups()
+    res = engine.ServerQueryExecutor().execute(q, [seg])
+    check_mode(res, kernel_mode)
+    groups = res.groups()
     cnt, s1, mx3, mn6, avg7 = groups[tuple(case["key"])]
     assert [cnt, s1, mx3, mn6, avg7[0], avg7[1]] == case["values"]
     _, og = oracle.execute(q, [bufs])
     assert_same_groups(groups, og)
 
 
-def test_golden_inter_group_by_order_by(engine, sv):
+def test_golden_inter_group_by_order_by(engine, sv, kernel_mode):
     bufs, seg = sv
     for case in EXP["inter_group_by"]["cases"]:
         q = ("SELECT " + ", ".join(case["group_by"]) + f", SUM({case['agg'][1]}) FROM testTable GROUP BY "
@@ -90,7 +105,7 @@ def test_golden_inter_group_by_order_by(engine, sv):
         assert [list(r) for r in rows] == case["rows"]
 
 
-def test_golden_inter_segment(engine, sv):
+def test_golden_inter_segment(engine, sv, kernel_mode):
     _, seg = sv
     ex = engine.ServerQueryExecutor()
     for case in EXP["inter"]["cases"]:
@@ -199,7 +214,7 @@ QUERIES = [
 
 @pytest.mark.parametrize("qi", range(len(QUERIES)))
 @pytest.mark.parametrize("n", [1, 1000, 250_007])
-def test_random_queries_vs_oracle(engine, qi, n):
+def test_random_queries_vs_oracle(engine, qi, n, kernel_mode):
     rng = np.random.default_rng(qi * 31 + n)
     bufs = random_segment(rng, n, inverted=("d1",))
     seg = engine.ImmutableSegment(bufs)
@@ -209,6 +224,7 @@ def test_random_queries_vs_oracle(engine, qi, n):
     fsum = {i for i, a in enumerate(qc.aggregations) if a.func in ("SUM", "AVG") and a.column == "r_double"}
     for inv in (True, False):
         res = engine.ServerQueryExecutor(inv).execute(qc, [seg])
+        check_mode(res, kernel_mode)
         nm, og = oracle.execute(qc, [bufs], inv)
         assert res.num_docs_matched() == nm
         got = res.groups()
@@ -217,7 +233,7 @@ def test_random_queries_vs_oracle(engine, qi, n):
         assert_same_groups(got, og, fsum)
 
 
-def test_multi_segment_different_dictionaries(engine):
+def test_multi_segment_different_dictionaries(engine, kernel_mode):
     """Segments with different dictionaries: the combine must key on values, not dictIds."""
     rng = np.random.default_rng(11)
     bufs = []
@@ -274,7 +290,7 @@ FILTERS = [
 
 @pytest.mark.parametrize("fi", range(len(FILTERS)))
 @pytest.mark.parametrize("n", [1, 1023, 1025, 200_003])
-def test_filter_doc_id_sets(engine, fi, n):
+def test_filter_doc_id_sets(engine, fi, n, kernel_mode):
     """FilterPlanNode -> docId set: bit-exact docIds (ascending) against the oracle's filter."""
     rng = np.random.default_rng(fi * 7 + n)
     bufs = random_segment(rng, n, inverted=("d1",))
@@ -290,7 +306,7 @@ def test_filter_doc_id_sets(engine, fi, n):
             assert np.array_equal(g, ids[:m])
 
 
-def test_golden_filter_doc_ids(engine, sv):
+def test_golden_filter_doc_ids(engine, sv, kernel_mode):
     """The reference FILTER over the golden segment selects 6129 docs; docIds match the oracle."""
     bufs, seg = sv
     from pinot_amd.query import parse_sql
