@@ -142,6 +142,15 @@ def main():
         assert set(r1) == set(o1) and all(r1[k][:3] == o1[k][:3] and r1[k][4] == o1[k][4] for k in o1)
         log("[check] HIP result == oracle on a 2M-row segment")
 
+    # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
+    # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_summary_bench40seg.json")
+    if os.path.exists(pmc) and res.kernel_info() == "jit":
+        d = json.load(open(pmc))["derived"]
+        traffic = (d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]) / d["rows_per_launch"] * rows_per_rank
+        traffic_src = "profiles/r01/pmc_summary_bench40seg.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-row)"
+
     out = None
     if rank == 0:
         cpu = None
@@ -181,7 +190,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "pinot_scan_jit" if res.kernel_info() == "jit" else "pamd::scan_kernel<4,true,false>",
                 "kernel_ms": avg_kernel_s * 1e3,
                 "bytes_per_row": datagen.BENCH_BYTES_PER_ROW,
