@@ -71,6 +71,8 @@ def lib():
         L.oracle_raw_read_f64.argtypes = [P, C.c_int32, I64]
         L.oracle_column_dict_ids.argtypes = [C.POINTER(OColumn), I64, I64, P]
         L.oracle_roaring_to_bitset.argtypes = [P, I64, P, I64]
+        L.oracle_lz4_decompress.restype = I64
+        L.oracle_lz4_decompress.argtypes = [P, I64, P, I64]
         L.oracle_inverted_to_bitset.argtypes = [P, C.c_int32, P, C.c_int32, P, I64]
         L.oracle_filter.restype = I64
         L.oracle_filter.argtypes = [C.POINTER(OColumn), I64, C.POINTER(OLeaf), C.c_int32, P]
@@ -156,6 +158,31 @@ def _raw_range(col: ColumnBuffers, p):
     return lo, hi
 
 
+def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
+    """The contiguous big-endian values of a raw forward index: the data region of PASS_THROUGH
+    chunks, or the LZ4 / LZ4_LENGTH_PREFIXED chunks decoded one by one
+    (BaseChunkForwardIndexReader.decompressChunk, BaseChunkForwardIndexReader.java:150-185)."""
+    h = parse_raw_fwd_header(cb.fwd)
+    fb = np.frombuffer(cb.fwd, dtype=np.uint8)
+    if h.compression == 0:
+        return fb[h.raw_data_start:].copy()
+    assert h.compression in (3, 4), h.compression
+    off_size = 4 if h.version <= 2 else 8
+    offs = np.frombuffer(cb.fwd, dtype=">i4" if off_size == 4 else ">i8", count=h.num_chunks,
+                         offset=h.data_header_start).astype(np.int64)
+    ends = np.r_[offs[1:], len(cb.fwd)]
+    total = cb.num_docs * h.size_of_entry
+    out = np.zeros(total + 16, dtype=np.uint8)
+    pos = 0
+    for s, e in zip(offs, ends):
+        src = fb[s + (4 if h.compression == 4 else 0):e].copy()
+        want = min(h.docs_per_chunk * h.size_of_entry, total - pos)
+        got = lib().oracle_lz4_decompress(src.ctypes.data, src.size, out[pos:].ctypes.data, want)
+        assert got == want, (got, want)
+        pos += want
+    return out
+
+
 class OracleSegment:
     """Host view of one segment's buffers in the oracle's column layout."""
 
@@ -173,8 +200,7 @@ class OracleSegment:
             oc.bits = cb.bits_per_element
             oc.cardinality = cb.cardinality
             if cb.encoding == "RAW":
-                h = parse_raw_fwd_header(cb.fwd)
-                buf = np.frombuffer(cb.fwd, dtype=np.uint8)[h.raw_data_start:].copy()
+                buf = raw_values_region(cb)
             else:
                 buf = np.frombuffer(cb.fwd, dtype=np.uint8).copy()
                 buf = np.concatenate([buf, np.zeros(16, np.uint8)])  # reads of the last byte's neighbour

@@ -153,6 +153,36 @@ static double value_f64(const oracle_column* c, int64_t doc) {
   }
 }
 
+/* LZ4 block decoding as lz4-java's LZ4FastDecompressor does it (org.lz4:lz4-java 1.11.0, pom.xml:186,
+ * third-party): the chunk decompressor behind ChunkCompressionType.LZ4
+ * (pinot-segment-local/.../io/compression/LZ4Decompressor.java). Returns bytes written or -1. */
+int64_t oracle_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  while (ip < n) {
+    uint32_t token = src[ip++];
+    int64_t lit = token >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do { if (ip >= n) return -1; b = src[ip++]; lit += b; } while (b == 255);
+    }
+    if (ip + lit > n || op + lit > cap) return -1;
+    for (int64_t k = 0; k < lit; k++) dst[op++] = src[ip++];
+    if (ip >= n) break;
+    if (ip + 2 > n) return -1;
+    int64_t off = src[ip] | (src[ip + 1] << 8);
+    ip += 2;
+    int64_t ml = token & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do { if (ip >= n) return -1; b = src[ip++]; ml += b; } while (b == 255);
+    }
+    ml += 4;
+    if (off == 0 || off > op || op + ml > cap) return -1;
+    for (int64_t k = 0; k < ml; k++, op++) dst[op] = dst[op - off];
+  }
+  return op;
+}
+
 /* ------------------------------------------------------------------ roaring */
 
 /* RoaringBitmap 1.6.14 portable deserialisation (org.roaringbitmap.buffer.ImmutableRoaringBitmap,

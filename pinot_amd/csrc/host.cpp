@@ -124,6 +124,46 @@ static std::u16string to_utf16(const std::string& s) {
 }
 static bool java_less(const std::string& a, const std::string& b) { return to_utf16(a) < to_utf16(b); }
 
+// LZ4 block decompression (lz4-java fastCompressor output, used by Pinot's LZ4 / LZ4_LENGTH_PREFIXED
+// chunk compressors: pinot-segment-local/.../io/compression/LZ4Decompressor.java). Returns the number
+// of bytes written or -1 on a malformed block.
+static int64_t lz4_block_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap) {
+  size_t ip = 0, op = 0;
+  while (ip < n) {
+    const uint32_t token = src[ip++];
+    size_t lit = token >> 4;
+    if (lit == 15) {
+      uint8_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (ip + lit > n || op + lit > cap) return -1;
+    memcpy(dst + op, src + ip, lit);
+    ip += lit;
+    op += lit;
+    if (ip >= n) break;  // last sequence: literals only
+    if (ip + 2 > n) return -1;
+    const size_t off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+    ip += 2;
+    size_t ml = token & 15;
+    if (ml == 15) {
+      uint8_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (off == 0 || off > op || op + ml > cap) return -1;
+    for (size_t k = 0; k < ml; ++k, ++op) dst[op] = dst[op - off];  // overlapping copies are byte-serial
+  }
+  return (int64_t)op;
+}
+
 struct RoaringContainerHost {
   uint32_t key, kind, count, pad;
   uint64_t offset;
@@ -347,14 +387,43 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
       const int32_t size = (int32_t)be32(fwd + 12);
       if (version < 2) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw index v%d (SNAPPY)", spec->name, version);
       const int32_t comp = (int32_t)be32(fwd + 20), dhs = (int32_t)be32(fwd + 24);
-      if (comp != 0)
-        return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d (only PASS_THROUGH is staged)", spec->name,
-                    comp);
       if (size != value_size(c->type)) return fail(PINOT_AMD_EINVAL, "column %s: entry size %d", spec->name, size);
-      const size_t raw_start = (size_t)dhs + (size_t)num_chunks * (version <= 2 ? 4 : 8);
+      const size_t off_size = version <= 2 ? 4 : 8;
+      const size_t raw_start = (size_t)dhs + (size_t)num_chunks * off_size;
       const size_t need = (size_t)nd * size;
-      if (spec->fwd_size < raw_start + need) return fail(PINOT_AMD_EINVAL, "column %s: raw data truncated", spec->name);
-      rc = c->fwd.alloc_copy(fwd + raw_start, need, kPadBytes);
+      if (comp == 0) {  // PASS_THROUGH: chunks are contiguous raw values
+        if (spec->fwd_size < raw_start + need) return fail(PINOT_AMD_EINVAL, "column %s: raw data truncated", spec->name);
+        rc = c->fwd.alloc_copy(fwd + raw_start, need, kPadBytes);
+      } else if (comp == 3 || comp == 4) {
+        // LZ4 / LZ4_LENGTH_PREFIXED chunks: decompressed once while staging, kept as contiguous values in HBM
+        const int32_t dpc = (int32_t)be32(fwd + 8);
+        std::vector<uint8_t> out(need + 16);
+        size_t op = 0;
+        for (int32_t ch = 0; ch < num_chunks; ++ch) {
+          const uint8_t* o = fwd + dhs + (size_t)ch * off_size;
+          const uint64_t start = off_size == 4 ? be32(o) : be64(o);
+          const uint64_t end = ch + 1 < num_chunks ? (off_size == 4 ? be32(o + 4) : be64(o + 8)) : spec->fwd_size;
+          if (start > end || end > spec->fwd_size) return fail(PINOT_AMD_EINVAL, "column %s: bad chunk offsets", spec->name);
+          const uint8_t* src = fwd + start;
+          size_t len = (size_t)(end - start);
+          if (comp == 4) {  // LZ4CompressorWithLength: 4-byte LE decompressed length first
+            if (len < 4) return fail(PINOT_AMD_EINVAL, "column %s: truncated LZ4 chunk", spec->name);
+            src += 4;
+            len -= 4;
+          }
+          const size_t want = std::min<size_t>((size_t)dpc * size, need - op);
+          const int64_t got = lz4_block_decompress(src, len, out.data() + op, want);
+          if (got != (int64_t)want)
+            return fail(PINOT_AMD_EINVAL, "column %s: LZ4 chunk %d decompressed to %lld of %zu bytes", spec->name, ch,
+                        (long long)got, want);
+          op += want;
+        }
+        if (op != need) return fail(PINOT_AMD_EINVAL, "column %s: decompressed %zu of %zu bytes", spec->name, op, need);
+        rc = c->fwd.alloc_copy(out.data(), need, kPadBytes);
+      } else {
+        return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d (PASS_THROUGH, LZ4 staged)", spec->name,
+                    comp);
+      }
       break;
     }
     default:

@@ -45,6 +45,8 @@ VALUE_SIZE = {INT: 4, LONG: 8, FLOAT: 4, DOUBLE: 8}
 
 # ChunkCompressionType (pinot-segment-spi/.../compression/ChunkCompressionType.java:22)
 PASS_THROUGH = 0
+LZ4 = 3
+LZ4_LENGTH_PREFIXED = 4
 
 # Default null values (FieldSpec.DEFAULT_*_NULL_VALUE_OF_*), used when ingesting nulls
 DEFAULT_DIMENSION_NULL = {INT: np.iinfo(np.int32).min, LONG: np.iinfo(np.int64).min,
@@ -113,7 +115,55 @@ def sorted_fwd_bytes(dict_ids: np.ndarray, cardinality: int) -> bytes:
 RAW_HEADER_INTS = 7
 
 
-def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:
+def lz4_block_compress(data: bytes) -> bytes:
+    """LZ4 block format (what lz4-java's fastCompressor emits): sequences of
+    token(lit_len:4 | match_len-4:4) [lit_len ext] literals [offset u16 LE] [match_len ext];
+    the last sequence is literals only and the last 5 bytes are always literals."""
+    n = len(data)
+    out = bytearray()
+    table = {}
+    anchor = 0
+    i = 0
+    limit = n - 12  # matches must end >= 5 bytes before the end (LZ4 end-of-block rules)
+
+    def put_len(x):
+        while x >= 255:
+            out.append(255)
+            x -= 255
+        out.append(x)
+
+    while i < limit:
+        key = data[i:i + 4]
+        cand = table.get(key)
+        table[key] = i
+        if cand is not None and i - cand <= 0xFFFF:
+            m = 4
+            while i + m < n - 5 and data[cand + m] == data[i + m]:
+                m += 1
+            lit = i - anchor
+            tok_l = min(lit, 15)
+            tok_m = min(m - 4, 15)
+            out.append((tok_l << 4) | tok_m)
+            if lit >= 15:
+                put_len(lit - 15)
+            out += data[anchor:i]
+            out += struct.pack("<H", i - cand)
+            if m - 4 >= 15:
+                put_len(m - 4 - 15)
+            i += m
+            anchor = i
+        else:
+            i += 1
+    lit = n - anchor
+    out.append(min(lit, 15) << 4)
+    if lit >= 15:
+        put_len(lit - 15)
+    out += data[anchor:]
+    return bytes(out)
+
+
+def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_per_chunk: int = 1000,
+                  compression: int = PASS_THROUGH) -> bytes:
     """FixedByteChunkForwardIndexWriter with PASS_THROUGH chunks.
 
     Header (BaseChunkForwardIndexWriter.java:131-165): version, numChunks,
@@ -123,7 +173,33 @@ def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_p
     Values are big-endian (java.nio.ByteBuffer default order).
     """
     data = np.ascontiguousarray(values).astype(_NP_BE[stored_type]).tobytes()
-    return raw_fwd_header(int(values.size), stored_type, version, docs_per_chunk) + data
+    if compression == PASS_THROUGH:
+        return raw_fwd_header(int(values.size), stored_type, version, docs_per_chunk) + data
+    if compression not in (LZ4, LZ4_LENGTH_PREFIXED):
+        raise NotImplementedError(f"compression {compression}")
+    # compressed chunks (BaseChunkForwardIndexWriter.writeChunk): offsets point at each compressed chunk
+    if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
+        docs_per_chunk = 1 << (docs_per_chunk - 1).bit_length()
+    n = int(values.size)
+    size = VALUE_SIZE[stored_type]
+    chunk_bytes = docs_per_chunk * size
+    chunks = []
+    for c in range(0, len(data), chunk_bytes):
+        raw = data[c:c + chunk_bytes]
+        blk = lz4_block_compress(raw)
+        if compression == LZ4_LENGTH_PREFIXED:  # LZ4CompressorWithLength: decompressed length, LE int
+            blk = struct.pack("<i", len(raw)) + blk
+        chunks.append(blk)
+    num_chunks = len(chunks)
+    off_size = 4 if version == 2 else 8
+    header_size = RAW_HEADER_INTS * 4 + num_chunks * off_size
+    hdr = struct.pack(">7i", version, num_chunks, docs_per_chunk, size, n, compression, RAW_HEADER_INTS * 4)
+    offs, pos = [], header_size
+    for blk in chunks:
+        offs.append(pos)
+        pos += len(blk)
+    hdr += struct.pack(">%d%s" % (num_chunks, "i" if off_size == 4 else "q"), *offs)
+    return hdr + b"".join(chunks)
 
 
 def raw_fwd_header(n: int, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:
@@ -306,14 +382,15 @@ class SegmentBuffers:
 
 
 def build_column(name: str, values, stored_type: str, dictionary: bool = True, inverted: bool = False,
-                 detect_sorted: bool = True, raw_version: int = 4) -> ColumnBuffers:
+                 detect_sorted: bool = True, raw_version: int = 4, compression: int = PASS_THROUGH) -> ColumnBuffers:
     """Create one column's buffers the way SegmentColumnarIndexCreator would for an SV column."""
     vals = np.asarray(values, dtype=object if stored_type == STRING else _NP_LE[stored_type])
     n = int(vals.size)
     if not dictionary:
         if stored_type == STRING:
             raise NotImplementedError("raw STRING forward index is outside the hot path")
-        return ColumnBuffers(name, stored_type, n, False, fwd=raw_fwd_bytes(vals, stored_type, raw_version))
+        return ColumnBuffers(name, stored_type, n, False,
+                             fwd=raw_fwd_bytes(vals, stored_type, raw_version, compression=compression))
     dvals, ids = build_dictionary(vals, stored_type)
     card = len(dvals)
     is_sorted = bool(detect_sorted and (n < 2 or np.all(np.diff(ids.astype(np.int64)) >= 0)))

@@ -146,3 +146,28 @@ def test_jit_codegen_compiles_for_gfx950():
     """The query-specialised kernels the planner generates compile with hipRTC (no device needed)."""
     from pinot_amd import _lib
     assert _lib.lib().pinot_amd_jit_selftest(0) == 0
+
+
+@pytest.mark.parametrize("comp", [S.LZ4, S.LZ4_LENGTH_PREFIXED])
+@pytest.mark.parametrize("t", [S.INT, S.LONG, S.DOUBLE])
+def test_lz4_chunks_roundtrip_through_oracle(comp, t):
+    """Raw forward index with LZ4 chunks (Pinot's default for raw dimension columns,
+    ForwardIndexType.getDefaultCompressionType) decodes to the original values."""
+    rng = np.random.default_rng(comp)
+    v = rng.integers(0, 40, 7001) if t != S.DOUBLE else rng.integers(0, 40, 7001) * 0.5
+    v = v.astype({S.INT: np.int32, S.LONG: np.int64, S.DOUBLE: np.float64}[t])
+    col = S.build_column("c", v, t, dictionary=False, compression=comp)
+    h = S.parse_raw_fwd_header(col.fwd)
+    assert h.compression == comp and len(col.fwd) < 7001 * S.VALUE_SIZE[t]
+    raw = oracle.raw_values_region(col)
+    got = np.frombuffer(raw[:v.nbytes].tobytes(), dtype=v.dtype.newbyteorder(">"))
+    assert np.array_equal(got, v)
+
+
+def test_lz4_known_block():
+    # literal-only block and a block with an overlapping match (offset 1, run of 'a')
+    assert oracle.lib().oracle_lz4_decompress(b"\x30abc", 4, (C.c_uint8 * 8)(), 8) == 3
+    dst = (C.c_uint8 * 32)()
+    blk = bytes([0x1F, ord("a"), 1, 0, 0x01, 0x50]) + b"bcdef"  # 'a' + match(off 1, len 4+15+1) + 'bcdef'
+    n = oracle.lib().oracle_lz4_decompress(blk, len(blk), dst, 32)
+    assert bytes(dst[:n]) == b"a" * 21 + b"bcdef"

@@ -317,3 +317,23 @@ def test_golden_filter_doc_ids(engine, sv, kernel_mode):
     ids = np.zeros(bufs.num_docs, dtype=np.int32)
     m = oracle.lib().oracle_bitset_to_doc_ids(bits.ctypes.data, bufs.num_docs, ids.ctypes.data)
     assert np.array_equal(got, ids[:m])
+
+
+@pytest.mark.parametrize("comp", [S.LZ4, S.LZ4_LENGTH_PREFIXED])
+def test_lz4_raw_columns_staged(engine, comp, kernel_mode):
+    """Raw dimension columns default to LZ4 chunks in Pinot; staging decodes them once into HBM."""
+    rng = np.random.default_rng(comp)
+    n = 50_001
+    bufs = S.build_segment("lz4", {
+        "d": (rng.integers(0, 300, n).astype(np.int32), S.INT, {}),
+        "ri": (rng.integers(-50, 50, n).astype(np.int32), S.INT, {"dictionary": False, "compression": comp}),
+        "rl": (rng.integers(0, 1 << 35, n), S.LONG, {"dictionary": False, "compression": comp}),
+        "rd": (rng.integers(0, 1000, n) * 0.125, S.DOUBLE, {"dictionary": False, "compression": comp}),
+    })
+    seg = engine.ImmutableSegment(bufs)
+    q = "SELECT d, COUNT(*), SUM(rl), MAX(rd), MIN(ri) FROM t WHERE ri BETWEEN -10 AND 30 AND rd > 20.5 GROUP BY d"
+    res = engine.ServerQueryExecutor().execute(q, [seg])
+    check_mode(res, kernel_mode)
+    nm, og = oracle.execute(q, [bufs])
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
