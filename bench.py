@@ -29,19 +29,32 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(seg_rows: int, seconds: float):
+def workloads():
+    """name -> (segment generator, query, algorithmic HBM bytes per row, description)."""
+    from pinot_amd import datagen
+    return {
+        "scan": (datagen.ad_segment, datagen.BENCH_QUERY, datagen.BENCH_BYTES_PER_ROW,
+                 "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE columns; "
+                 "filter+group-by query"),
+        "highcard": (datagen.highcard_segment, datagen.HIGHCARD_QUERY, datagen.HIGHCARD_BYTES_PER_ROW,
+                     "configs[3]: high-cardinality GROUP BY on 2 dims (1M groups), SUM/COUNT/MIN/MAX, "
+                     "100 segments x 10M rows per GPU (8B rows on 8 GPUs), RCCL merge of the group tables"),
+    }
+
+
+def cpu_baseline(workload: str, seg_rows: int, seconds: float):
     """Time the CPU oracle (scalar C port of the reference path, 1 core) on freshly generated
     segments of the same workload until `seconds` of CPU work have run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from pinot_amd import datagen
+    gen, query, _, _ = workloads()[workload]
     rows = 0
     t_cpu = 0.0
     k = 0
     while t_cpu < seconds and k < 64:
-        bufs = datagen.ad_segment(f"cpu{k}", seg_rows, seed=10_000 + k)
+        bufs = gen(f"cpu{k}", seg_rows, seed=10_000 + k)
         t0 = time.perf_counter()
-        oracle.execute(datagen.BENCH_QUERY, [bufs])
+        oracle.execute(query, [bufs])
         t_cpu += time.perf_counter() - t0
         rows += seg_rows
         k += 1
@@ -53,6 +66,7 @@ def cpu_baseline(seg_rows: int, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", default="scan", choices=["scan", "highcard"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segments", type=int, default=100)
@@ -65,6 +79,8 @@ def main():
     import torch
     import torch.distributed as dist
     from pinot_amd import datagen, dist as pdist, engine
+    from pinot_amd.query import parse_sql
+    gen, query, bytes_per_row, workload_desc = workloads()[args.workload]
 
     rank, world, local = pdist.init_distributed()
     torch.cuda.set_device(local)
@@ -75,7 +91,7 @@ def main():
     t0 = time.time()
     segs = []
     for i in range(args.segments):
-        bufs = datagen.ad_segment(f"adAnalytics_{rank}_{i}", args.rows, seed=rank * 100_003 + i)
+        bufs = gen(f"{args.workload}_{rank}_{i}", args.rows, seed=rank * 100_003 + i)
         segs.append(engine.ImmutableSegment(bufs))
         del bufs
         if i % 20 == 19:
@@ -85,7 +101,7 @@ def main():
 
     stream = torch.cuda.current_stream()
     ex = engine.ServerQueryExecutor()
-    res = ex.execute(datagen.BENCH_QUERY, segs, stream=stream)
+    res = ex.execute(query, segs, stream=stream)
     scratch = None
 
     def step():
@@ -119,7 +135,7 @@ def main():
     total_rows = rows_per_rank * world * args.steps
     value = total_rows / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    alg_bytes = rows_per_rank * datagen.BENCH_BYTES_PER_ROW   # per launch (one launch = all segments)
+    alg_bytes = rows_per_rank * bytes_per_row   # per launch (one launch = all segments)
     achieved = alg_bytes / avg_kernel_s / 1e9
 
     groups = res.groups()
@@ -136,17 +152,25 @@ def main():
     if args.check and rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        one = datagen.ad_segment("check", min(args.rows, 2_000_000), seed=424242)
-        r1 = ex.execute(datagen.BENCH_QUERY, [engine.ImmutableSegment(one)]).groups()
-        _, o1 = oracle.execute(datagen.BENCH_QUERY, [one])
-        assert set(r1) == set(o1) and all(r1[k][:3] == o1[k][:3] and r1[k][4] == o1[k][4] for k in o1)
+        one = gen("check", min(args.rows, 2_000_000), seed=424242)
+        r1 = ex.execute(query, [engine.ImmutableSegment(one)]).groups()
+        _, o1 = oracle.execute(query, [one])
+        assert set(r1) == set(o1), "group keys differ"
+        qc = parse_sql(query)
+        for k in o1:
+            for i, a in enumerate(qc.aggregations):
+                g, e = r1[k][i], o1[k][i]
+                if a.func == "SUM" and isinstance(e, float) and e != int(e):
+                    assert abs(g - e) <= 1e-12 * abs(e), (k, a.name, g, e)
+                else:
+                    assert g == e, (k, a.name, g, e)
         log("[check] HIP result == oracle on a 2M-row segment")
 
     # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
     # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01", "pmc_summary_bench40seg.json")
-    if os.path.exists(pmc) and res.kernel_info() == "jit":
+    if os.path.exists(pmc) and res.kernel_info() == "jit" and args.workload == "scan":
         d = json.load(open(pmc))["derived"]
         traffic = (d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]) / d["rows_per_launch"] * rows_per_rank
         traffic_src = "profiles/r01/pmc_summary_bench40seg.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-row)"
@@ -156,7 +180,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             log("[rank 0] timing the CPU baseline ...")
-            cpu = cpu_baseline(min(args.rows, 10_000_000), args.cpu_seconds)
+            cpu = cpu_baseline(args.workload, min(args.rows, 10_000_000), args.cpu_seconds)
         out = {
             "metric": "rows scanned/sec + achieved HBM GB/s, filter+group-by query, 1/2/4/8 GPUs",
             "value": value,
@@ -171,9 +195,8 @@ def main():
             "dtype": "int32/int64/f64",
             "data": "synthetic (device-generated segments in Pinot's on-disk formats)",
             "config": {
-                "workload": "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE "
-                            "columns; filter+group-by query",
-                "query": datagen.BENCH_QUERY,
+                "workload": workload_desc,
+                "query": query,
                 "segments_per_gpu": args.segments,
                 "rows_per_segment": args.rows,
                 "rows_per_gpu": rows_per_rank,
@@ -192,9 +215,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "pinot_scan_jit" if res.kernel_info() == "jit" else "pamd::scan_kernel<4,true,false>",
+                "kernel": {"jit": "pinot_scan_jit", "jit-partitioned": "pinot_part_count+scatter+agg"}.get(
+                    res.kernel_info(), "pamd::scan_kernel<4,true,false>"),
                 "kernel_ms": avg_kernel_s * 1e3,
-                "bytes_per_row": datagen.BENCH_BYTES_PER_ROW,
+                "bytes_per_row": bytes_per_row,
             },
             "cpu_baseline": cpu,
         }

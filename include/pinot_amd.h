@@ -202,6 +202,13 @@ int pinot_amd_result_destroy(pinot_amd_result* r);
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out);
 /* Number of groups with >= 1 matching doc (1 for an aggregation-only query). */
 int pinot_amd_result_num_groups(pinot_amd_result* r, int64_t* h_out);
+/* numGroupsLimitReached (DefaultGroupByExecutor / GroupByResultsBlock metadata): 1 when the merged
+ * result holds more groups than the query's numGroupsLimit. Pinot drops the groups a segment first
+ * sees after its limit is reached (DictionaryBasedGroupKeyGenerator.java:352-360, first-seen docId
+ * order); this library keeps every group, so its results equal Pinot's exactly when this is 0 —
+ * set the numGroupsLimit query option above the expected group count for high-cardinality GROUP BY.
+ * Conservative: the merged count bounds every segment's count. */
+int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_out);
 /* Fetch up to cap groups: h_keys[g*num_group_by + j] = group-by column j's value as int64 (INT/LONG),
  * its double bits (FLOAT/DOUBLE) or its index into the merged STRING dictionary
  * (pinot_amd_result_string_key); h_values[g*num_aggs + a] = final result as double

@@ -62,6 +62,23 @@ struct DevSegment {
   DevLeaf leaves[kMaxLeaves];
 };
 
+// Partitioned GROUP BY (key spaces too large for an LDS table): the scan emits one record per
+// matching doc into key-range partitions, then each partition is aggregated in LDS.
+//   count pass:   hist[p * grid + block] = matching docs of `block` whose key falls in partition p
+//   scan:         offs[p * grid + block] = exclusive prefix within partition p; part_begin = prefix
+//                 of partition totals (part_begin[nparts] = all records)
+//   scatter pass: record r of partition p at part_begin[p] + offs[..] + running index:
+//                 keys[r] = key & (2^key_shift - 1), vals[j][r] = value of record column j
+//   agg pass:     one LDS table of 2^key_shift keys per partition, flushed with global atomics
+struct DevPartition {
+  int32_t nparts, key_shift;
+  uint32_t* hist;
+  int64_t* offs;
+  int64_t* part_begin;
+  uint16_t* keys;
+  void* vals[kMaxAcc];
+};
+
 // Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the
 // kernel's per-slot loop indexes the decoded values with compile-time indices only.
 struct DevQuery {

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -38,6 +39,8 @@ hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const i
                                  int32_t* out, hipStream_t st);
 hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const int32_t* sel, int32_t nsel,
                                  int64_t num_docs, uint64_t* bitset, hipStream_t st);
+hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
+                                    int64_t* d_part_begin, hipStream_t st);
 }  // namespace pamd
 
 using namespace pamd;
@@ -683,6 +686,14 @@ struct pinot_amd_result {
   JitKernel* jit = nullptr;      // query-specialised kernel (nullptr: AOT scan_kernel)
   std::string jit_status;        // why the AOT kernel runs, if it does
   size_t shmem = 0;
+  // partitioned GROUP BY (JIT only): count -> offsets -> scatter -> per-partition LDS aggregation
+  int64_t num_groups_limit = 100000;
+  bool partitioned = false;
+  DevPartition part{};
+  DevBuf hist, offs, part_begin, rec_keys;
+  std::vector<std::unique_ptr<DevBuf>> rec_vals;
+  int agg_grid = 1;
+  size_t shmem_scatter = 0, shmem_agg = 0;
   ~pinot_amd_result() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -982,12 +993,26 @@ static int run_plan(pinot_amd_result* r) {
   HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
   if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
   HIP_OK(hipEventRecord(r->ev0, st));
-  if (r->jit) {
+  if (r->jit && r->partitioned) {
+    const DevSegment* segs = (const DevSegment*)r->d_segs.p;
+    uint64_t* acc = (uint64_t*)r->acc.p;
+    uint64_t* const* bits = nullptr;
+    unsigned long long* matched = (unsigned long long*)r->matched.p;
+    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem, st, args,
+                                 nullptr));
+    HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, r->grid, r->part.offs, r->part.part_begin, st));
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn_scatter, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem_scatter,
+                                 st, args, nullptr));
+    void* agg_args[] = {(void*)&r->part, (void*)&acc};
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn_agg, (unsigned)r->agg_grid, 1, 1, 1024, 1, 1, (unsigned)r->shmem_agg, st,
+                                 agg_args, nullptr));
+  } else if (r->jit) {
     const DevSegment* segs = (const DevSegment*)r->d_segs.p;
     uint64_t* acc = (uint64_t*)r->acc.p;
     uint64_t* const* bits = r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p;
     unsigned long long* matched = (unsigned long long*)r->matched.p;
-    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched};
+    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
     HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem, st, args,
                                  nullptr));
   } else {
@@ -1100,6 +1125,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
 
   // ---- group-by key space ----
   r->num_group_by = (int32_t)Q.group_by.size();
+  r->num_groups_limit = Q.num_groups_limit;
   int64_t num_keys = 1;
   std::vector<std::vector<int32_t>> remaps;  // [g][seg] handled below
   for (auto& g : Q.group_by) {
@@ -1267,13 +1293,58 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     jp.lds = q.lds_keys > 0;
     jp.bitset = filter_only;
     jp.aggregate = q.nacc > 0;
+    // key space too large for an LDS table: partition the matching docs by key range and
+    // aggregate each partition in LDS (per-lane HBM atomics on random keys run ~17x below the
+    // coalesced atomic rate). Keys per partition: the largest power of two whose nacc tables fit
+    // in one workgroup's LDS (gfx950: 160 KiB); local keys are 16-bit.
+    int lds_max = 0;
+    {
+      int dev = 0;
+      HIP_OK(hipGetDevice(&dev));
+      if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) lds_max = 65536;
+      lds_max = std::min(lds_max, 160 * 1024);
+    }
+    const char* pe = getenv("PINOT_AMD_PARTITIONED");
+    const bool allow_part = !(pe && strcmp(pe, "0") == 0);
+    if (ok && allow_part && !filter_only && q.nacc > 0 && !jp.lds && !Q.group_by.empty()) {
+      int shift = 16;
+      while (shift > 6 && (int64_t)q.nacc * ((int64_t)1 << shift) * 8 > lds_max) --shift;
+      const int64_t nparts = (num_keys + ((int64_t)1 << shift) - 1) >> shift;
+      if ((int64_t)q.nacc * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
+        jp.partitioned = true;
+        jp.key_shift = shift;
+        jp.nparts = (int)nparts;
+        for (auto& a : jp.accs)
+          if (std::find(jp.val_slots.begin(), jp.val_slots.end(), a.slot) == jp.val_slots.end())
+            jp.val_slots.push_back(a.slot);
+      }
+    }
     if (ok) {
       r->jit = jit_get(jp, &r->jit_status);
     } else {
       r->jit_status = "segments disagree on a column's encoding";
     }
+    if (r->jit && jp.partitioned) {
+      r->partitioned = true;
+      r->part.nparts = jp.nparts;
+      r->part.key_shift = jp.key_shift;
+      r->shmem_scatter = (size_t)jp.nparts * 8;
+      r->shmem_agg = (size_t)q.nacc * ((size_t)1 << jp.key_shift) * 8;
+      int64_t total_docs = 0;
+      for (auto* s : segs) total_docs += s->num_docs;
+      rc = r->rec_keys.alloc((size_t)total_docs * 2 + 256);
+      for (size_t j = 0; rc == 0 && j < jp.val_slots.size(); ++j) {
+        auto b = std::make_unique<DevBuf>();
+        rc = b->alloc((size_t)total_docs * jit_val_size(jp.slots[jp.val_slots[j]]) + 256);
+        r->part.vals[j] = b->p;
+        r->rec_vals.push_back(std::move(b));
+      }
+      if (rc) return rc;
+      r->part.keys = (uint16_t*)r->rec_keys.p;
+    }
   }
   r->shmem = q.lds_keys > 0 ? (size_t)lds_bytes : 0;
+  if (r->partitioned) r->shmem = (size_t)r->part.nparts * 4;
 
   // persistent grid: enough blocks to fill every CU at the occupancy the LDS table allows
   int dev = 0, cus = 256;
@@ -1281,7 +1352,19 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   // resident blocks per CU (VGPR / LDS limited): a larger grid would only queue a second, tail-heavy wave
   int per_cu = 1;
-  if (r->jit) {
+  if (r->jit && r->partitioned) {
+    // count and scatter passes must share the block -> tile mapping: size for the scatter pass
+    int nb = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn_scatter, kBlock, r->shmem_scatter) !=
+            hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = nb;
+    int na = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&na, r->jit->fn_agg, 1024, r->shmem_agg) != hipSuccess ||
+        na < 1)
+      na = 1;
+    r->agg_grid = cus * na;
+  } else if (r->jit) {
     int nb = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock, r->shmem) != hipSuccess || nb < 1)
       nb = 1;
@@ -1292,6 +1375,16 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   int64_t grid = (int64_t)cus * per_cu;
   if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
   r->grid = (int)grid;
+  if (r->partitioned) {
+    const size_t cells = (size_t)r->part.nparts * (size_t)grid;
+    rc = r->hist.alloc(cells * 4);
+    if (!rc) rc = r->offs.alloc(cells * 8);
+    if (!rc) rc = r->part_begin.alloc(((size_t)r->part.nparts + 1) * 8);
+    if (rc) return rc;
+    r->part.hist = (uint32_t*)r->hist.p;
+    r->part.offs = (int64_t*)r->offs.p;
+    r->part.part_begin = (int64_t*)r->part_begin.p;
+  }
   HIP_OK(hipEventCreate(&r->ev0));
   HIP_OK(hipEventCreate(&r->ev1));
   rc = run_plan(r);
@@ -1343,7 +1436,7 @@ int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
 const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
   if (!r) return "";
   static thread_local std::string info;
-  info = r->jit ? "jit" : ("aot: " + r->jit_status);
+  info = r->jit ? (r->partitioned ? "jit-partitioned" : "jit") : ("aot: " + r->jit_status);
   return info.c_str();
 }
 
@@ -1362,6 +1455,15 @@ static int fetch_acc(pinot_amd_result* r, std::vector<uint64_t>* h) {
   if (r->q.nacc == 0) return 0;
   HIP_OK(hipMemcpyAsync(h->data(), r->acc.p, h->size() * 8, hipMemcpyDeviceToHost, r->stream));
   HIP_OK(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
+int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_out) {
+  if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_groups_limit_reached: bad arguments");
+  int64_t g = 0;
+  int rc = pinot_amd_result_num_groups(r, &g);
+  if (rc) return rc;
+  *h_out = (r->num_group_by > 0 && g > r->num_groups_limit) ? 1 : 0;
   return 0;
 }
 

@@ -35,12 +35,22 @@ struct JitPlan {
   bool lds = false;
   bool bitset = false;
   bool aggregate = true;
+  // partitioned GROUP BY (DevPartition): count / scatter / LDS-aggregate kernels instead of one scan
+  bool partitioned = false;
+  int key_shift = 0;           // keys per partition = 2^key_shift
+  int nparts = 0;
+  std::vector<int> val_slots;  // record value columns (slots read by accumulators)
 };
 struct JitKernel {
   std::vector<char> image;
   hipModule_t module = nullptr;
-  hipFunction_t fn = nullptr;
+  hipFunction_t fn = nullptr;          // pinot_scan_jit, or the partition count pass
+  hipFunction_t fn_scatter = nullptr;  // partitioned: scatter pass
+  hipFunction_t fn_agg = nullptr;      // partitioned: LDS aggregation of the partitions
 };
+// record value column j of a partitioned plan: C type of the stored value
+const char* jit_val_ctype(const JitSlot& s);
+int jit_val_size(const JitSlot& s);
 
 std::string jit_shape_key(const JitPlan& p);
 std::string jit_generate(const JitPlan& p);

@@ -618,6 +618,36 @@ __global__ void exclusive_scan_kernel(int64_t* counts, int64_t n, int64_t* total
   if (threadIdx.x == 0) *total = carry;
 }
 
+// Partitioned GROUP BY offsets (DevPartition): row p of hist holds the per-block record counts of
+// partition p; one block per row turns it into exclusive per-block offsets and the row total.
+__global__ void partition_row_scan_kernel(const uint32_t* hist, int64_t nblocks, int64_t* offs, int64_t* row_total) {
+  __shared__ int64_t wtot[kBlock / 64];
+  __shared__ int64_t carry;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = blockIdx.x;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nblocks; base += kBlock) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t x = i < nblocks ? (int64_t)hist[row * nblocks + i] : 0;
+    int64_t incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int w = 0; w < wave; ++w) before += wtot[w];
+    if (i < nblocks) offs[row * nblocks + i] = before + incl - x;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) row_total[row] = carry;
+}
+
 // pass 3: each wave compacts 64 words (4096 docs) per step with ballot + mbcnt style prefix sums
 __global__ void bitset_compact_kernel(const uint64_t* bits, int64_t nwords, const int64_t* chunk_offsets,
                                       int32_t* out) {
@@ -816,6 +846,16 @@ hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const in
   hipLaunchKernelGGL(roaring_expand_kernel, dim3((unsigned)nsel), dim3(kBlock), 0, st, inv,
                      reinterpret_cast<const RoaringContainer*>(conts), sel, num_docs,
                      reinterpret_cast<unsigned long long*>(bitset));
+  return hipGetLastError();
+}
+
+hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
+                                    int64_t* d_part_begin, hipStream_t st) {
+  if (nparts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(partition_row_scan_kernel, dim3((unsigned)nparts), dim3(kBlock), 0, st, d_hist, nblocks, d_offs,
+                     d_part_begin);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, d_part_begin, (int64_t)nparts,
+                     d_part_begin + nparts);
   return hipGetLastError();
 }
 

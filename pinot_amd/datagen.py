@@ -69,3 +69,40 @@ BENCH_QUERY = ("SELECT daysSinceEpoch, COUNT(*), SUM(clicks), SUM(impressions), 
 # Algorithmic HBM bytes per row of BENCH_QUERY: every referenced column is read once
 # (9-bit daysSinceEpoch + 4 B clicks + 8 B impressions + 8 B cost); group accumulators stay in LDS.
 BENCH_BYTES_PER_ROW = S.num_bits_per_value(NUM_DAYS - 1) / 8.0 + 4 + 8 + 8
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE.json configs[3]: high-cardinality GROUP BY on 2 dimensions (~1M groups)
+HC_CARD = 1000             # dimA x dimB = 1,000,000 groups
+
+
+def highcard_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+    """Segment of the high-cardinality table: two fixed-bit dictionary-encoded dimensions of
+    cardinality 1000 (10 bits each) and raw INT / LONG / DOUBLE metrics."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = num_docs
+    cols = {}
+    for cname, base in (("dimA", 1_000_000), ("dimB", 5_000_000)):
+        ids = torch.randint(0, HC_CARD, (n,), generator=g, device=device, dtype=torch.int32)
+        ids[:HC_CARD] = torch.arange(HC_CARD, device=device, dtype=torch.int32)
+        bits = S.num_bits_per_value(HC_CARD - 1)
+        dvals = np.arange(base, base + 7 * HC_CARD, 7, dtype=np.int32)
+        cols[cname] = S.ColumnBuffers(cname, S.INT, n, True, False, HC_CARD, bits, _fixed_bit(ids, bits),
+                                      S.dictionary_bytes(dvals, S.INT), None, dvals)
+    met_int = torch.randint(0, 1000, (n,), generator=g, device=device, dtype=torch.int32)
+    met_long = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, device=device, dtype=torch.int64)
+    met_double = torch.randn((n,), generator=g, device=device, dtype=torch.float64) * 1000.0
+    for cname, t, st, size in (("metInt", met_int, S.INT, 4), ("metLong", met_long, S.LONG, 8),
+                               ("metDouble", met_double, S.DOUBLE, 8)):
+        cols[cname] = S.ColumnBuffers(cname, st, n, False, fwd=S.raw_fwd_header(n, st) + _be_bytes(t, size))
+    torch.cuda.synchronize()
+    return S.SegmentBuffers(name, n, cols)
+
+
+# SUM / COUNT / MIN / MAX grouped by both dimensions; numGroupsLimit raised above the key space so
+# Pinot keeps every group (its default, 100000, would trim)
+HIGHCARD_QUERY = ("SET numGroupsLimit = 2000000; SELECT dimA, dimB, COUNT(*), SUM(metInt), MIN(metLong), "
+                  "MAX(metDouble) FROM highCard WHERE metInt < 900 GROUP BY dimA, dimB")
+HIGHCARD_BYTES_PER_ROW = 2 * S.num_bits_per_value(HC_CARD - 1) / 8.0 + 4 + 8 + 8

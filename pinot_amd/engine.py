@@ -171,8 +171,15 @@ class QueryResult:
         check(lib().pinot_amd_result_num_docs_matched(self._h, C.byref(out)), "num_docs_matched")
         return out.value
 
+    def num_groups_limit_reached(self) -> bool:
+        """GroupByResultsBlock.isNumGroupsLimitReached: more groups than the numGroupsLimit option."""
+        out = C.c_int32()
+        check(lib().pinot_amd_result_num_groups_limit_reached(self._h, C.byref(out)), "num_groups_limit_reached")
+        return bool(out.value)
+
     def kernel_info(self) -> str:
-        """'jit' when the query-specialised kernel runs, else 'aot: <reason>'."""
+        """'jit' when the query-specialised kernel runs ('jit-partitioned' for the partitioned
+        high-cardinality GROUP BY), else 'aot: <reason>'."""
         return lib().pinot_amd_result_kernel_info(self._h).decode()
 
     def last_kernel_ms(self) -> float:

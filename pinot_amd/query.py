@@ -330,9 +330,39 @@ class _Parser:
         raise ValueError(f"unsupported operator {op}")
 
 
+_SET_OPTION = re.compile(r"^\s*SET\s+([A-Za-z_][A-Za-z0-9_]*)\s*=\s*'?([^;']*)'?\s*;", re.IGNORECASE)
+_OPTION_CLAUSE = re.compile(r"\bOPTION\s*\(([^)]*)\)\s*;?\s*$", re.IGNORECASE)
+
+
+def _query_options(sql: str):
+    """Query options from ``SET key = value;`` prefixes (multi-stage style, CalciteSqlParser) and a
+    trailing legacy ``OPTION(key=value, ...)`` clause; returns (remaining SQL, options)."""
+    opts = {}
+    while True:
+        m = _SET_OPTION.match(sql)
+        if not m:
+            break
+        opts[m.group(1)] = m.group(2).strip()
+        sql = sql[m.end():]
+    m = _OPTION_CLAUSE.search(sql)
+    if m:
+        for kv in m.group(1).split(","):
+            if kv.strip():
+                k, _, v = kv.partition("=")
+                opts[k.strip()] = v.strip().strip("'")
+        sql = sql[:m.start()]
+    return sql, opts
+
+
 def parse_sql(sql: str) -> QueryContext:
-    """Compile a Pinot SQL query of the supported subset into a QueryContext."""
-    return _Parser(sql).query()
+    """Compile a Pinot SQL query of the supported subset into a QueryContext. The numGroupsLimit
+    query option (QueryOptionsUtils.getNumGroupsLimit) is honoured; other options are ignored."""
+    sql, opts = _query_options(sql)
+    qc = _Parser(sql).query()
+    for k, v in opts.items():
+        if k.lower() == "numgroupslimit":
+            qc.num_groups_limit = int(v)
+    return qc
 
 
 # ---------------------------------------------------------------------------------------- reduce
