@@ -67,16 +67,17 @@ struct DevSegment {
 //   count pass:   hist[p * grid + block] = matching docs of `block` whose key falls in partition p
 //   scan:         offs[p * grid + block] = exclusive prefix within partition p; part_begin = prefix
 //                 of partition totals (part_begin[nparts] = all records)
-//   scatter pass: record r of partition p at part_begin[p] + offs[..] + running index:
-//                 keys[r] = key & (2^key_shift - 1), vals[j][r] = value of record column j
+//   scatter pass: record r of partition p at part_begin[p] + offs[..] + running index, staged per
+//                 partition in LDS and written out in runs; a record is `rec_bytes` bytes at
+//                 rec + r * rec_bytes: u32 local key (key & (2^key_shift - 1)), then the values of
+//                 the accumulated columns (4-byte values first, then 8-byte values, 8-B aligned)
 //   agg pass:     one LDS table of 2^key_shift keys per partition, flushed with global atomics
 struct DevPartition {
   int32_t nparts, key_shift;
   uint32_t* hist;
   int64_t* offs;
   int64_t* part_begin;
-  uint16_t* keys;
-  void* vals[kMaxAcc];
+  uint8_t* rec;
 };
 
 // Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the

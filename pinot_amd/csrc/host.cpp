@@ -690,8 +690,8 @@ struct pinot_amd_result {
   int64_t num_groups_limit = 100000;
   bool partitioned = false;
   DevPartition part{};
-  DevBuf hist, offs, part_begin, rec_keys;
-  std::vector<std::unique_ptr<DevBuf>> rec_vals;
+  DevBuf hist, offs, part_begin, rec;
+  int rec_bytes = 0, stage_cap = 0;
   int agg_grid = 1;
   size_t shmem_scatter = 0, shmem_agg = 0;
   ~pinot_amd_result() {
@@ -999,11 +999,12 @@ static int run_plan(pinot_amd_result* r) {
     uint64_t* const* bits = nullptr;
     unsigned long long* matched = (unsigned long long*)r->matched.p;
     void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem, st, args,
-                                 nullptr));
-    HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, r->grid, r->part.offs, r->part.part_begin, st));
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn_scatter, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem_scatter,
-                                 st, args, nullptr));
+    const unsigned pt = (unsigned)(kBlock * kPartSub);
+    const unsigned count_grid = (unsigned)(r->grid * kPartCountRatio);
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn, count_grid, 1, 1, pt, 1, 1, (unsigned)r->shmem, st, args, nullptr));
+    HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, count_grid, r->part.offs, r->part.part_begin, st));
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn_scatter, (unsigned)r->grid, 1, 1, pt, 1, 1, (unsigned)r->shmem_scatter, st,
+                                 args, nullptr));
     void* agg_args[] = {(void*)&r->part, (void*)&acc};
     HIP_OK(hipModuleLaunchKernel(r->jit->fn_agg, (unsigned)r->agg_grid, 1, 1, 1024, 1, 1, (unsigned)r->shmem_agg, st,
                                  agg_args, nullptr));
@@ -1268,7 +1269,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (int sl = 0; sl < nslots && ok; ++sl) {
       const int enc = r->hsegs[0].cols[sl].enc;
       for (int si = 1; si < n; ++si) ok &= r->hsegs[si].cols[sl].enc == enc;
-      jp.slots.push_back({enc, r->hsegs[0].cols[sl].type});
+      JitSlot js{enc, r->hsegs[0].cols[sl].type, 0};
+      if (enc == ENC_FIXED_BIT) {
+        // bit width shared by the whole batch (and <= 15): decode with compile-time shifts
+        js.bits = r->hsegs[0].cols[sl].bits;
+        for (int si = 1; si < n; ++si)
+          if (r->hsegs[si].cols[sl].bits != js.bits || r->hsegs[si].cols[sl].enc != enc) js.bits = 0;
+        if (js.bits > 15) js.bits = 0;
+        if (const char* gb = getenv("PINOT_AMD_GENERIC_BITS"))
+          if (strcmp(gb, "1") == 0) js.bits = 0;
+      }
+      jp.slots.push_back(js);
     }
     for (size_t k = 0; k < order.size(); ++k) {
       JitLeaf jl{pred_slot[order[k]], Q.preds[order[k]].clause, r->hsegs[0].leaves[k].negate, 0u};
@@ -1317,6 +1328,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         for (auto& a : jp.accs)
           if (std::find(jp.val_slots.begin(), jp.val_slots.end(), a.slot) == jp.val_slots.end())
             jp.val_slots.push_back(a.slot);
+        jit_layout_records(&jp);
+        // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a
+        // run is too short to pay for the staging round trip and records are written directly
+        int cap = 64;
+        while (cap >= 4 && jit_scatter_lds(jp, cap) > (size_t)lds_max) --cap;
+        jp.stage_cap = cap >= 4 ? cap : 0;
+        if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
       }
     }
     if (ok) {
@@ -1328,19 +1346,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       r->partitioned = true;
       r->part.nparts = jp.nparts;
       r->part.key_shift = jp.key_shift;
-      r->shmem_scatter = (size_t)jp.nparts * 8;
+      r->shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
       r->shmem_agg = (size_t)q.nacc * ((size_t)1 << jp.key_shift) * 8;
       int64_t total_docs = 0;
       for (auto* s : segs) total_docs += s->num_docs;
-      rc = r->rec_keys.alloc((size_t)total_docs * 2 + 256);
-      for (size_t j = 0; rc == 0 && j < jp.val_slots.size(); ++j) {
-        auto b = std::make_unique<DevBuf>();
-        rc = b->alloc((size_t)total_docs * jit_val_size(jp.slots[jp.val_slots[j]]) + 256);
-        r->part.vals[j] = b->p;
-        r->rec_vals.push_back(std::move(b));
-      }
+      rc = r->rec.alloc((size_t)total_docs * jp.rec_bytes + 256);
       if (rc) return rc;
-      r->part.keys = (uint16_t*)r->rec_keys.p;
+      r->part.rec = (uint8_t*)r->rec.p;
+      r->rec_bytes = jp.rec_bytes;
+      r->stage_cap = jp.stage_cap;
     }
   }
   r->shmem = q.lds_keys > 0 ? (size_t)lds_bytes : 0;
@@ -1355,8 +1369,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   if (r->jit && r->partitioned) {
     // count and scatter passes must share the block -> tile mapping: size for the scatter pass
     int nb = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn_scatter, kBlock, r->shmem_scatter) !=
-            hipSuccess || nb < 1)
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn_scatter, kBlock * kPartSub,
+                                                           r->shmem_scatter) != hipSuccess || nb < 1)
       nb = 1;
     per_cu = nb;
     int na = 0;
@@ -1374,9 +1388,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   int64_t grid = (int64_t)cus * per_cu;
   if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
+  if (r->partitioned && grid * kPartSub > tiles) grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
   r->grid = (int)grid;
   if (r->partitioned) {
-    const size_t cells = (size_t)r->part.nparts * (size_t)grid;
+    const size_t cells = (size_t)r->part.nparts * (size_t)grid * kPartCountRatio;
     rc = r->hist.alloc(cells * 4);
     if (!rc) rc = r->offs.alloc(cells * 8);
     if (!rc) rc = r->part_begin.alloc(((size_t)r->part.nparts + 1) * 8);

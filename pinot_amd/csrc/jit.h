@@ -10,9 +10,13 @@
 
 namespace pamd {
 
+constexpr int kPartSub = 4;  // partition count / scatter blocks: 4 x 256 threads (one block per CU)
+constexpr int kPartCountRatio = 2;  // count-pass blocks per scatter-pass block (count needs little LDS)
+
 struct JitSlot {
-  int enc;   // ENC_* (the same in every segment of the batch)
-  int type;  // T_* value type
+  int enc;       // ENC_* (the same in every segment of the batch)
+  int type;      // T_* value type
+  int bits = 0;  // FIXED_BIT: bit width when every segment of the batch agrees (<= 15), else 0
 };
 struct JitLeaf {
   int slot;        // -1: reads no column (docId range / bitset / constant)
@@ -40,7 +44,14 @@ struct JitPlan {
   int key_shift = 0;           // keys per partition = 2^key_shift
   int nparts = 0;
   std::vector<int> val_slots;  // record value columns (slots read by accumulators)
+  std::vector<int> val_off;    // byte offset of each value column in a record (key u32 at 0)
+  int rec_bytes = 0;           // record size, multiple of 8
+  int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
 };
+// record layout of a partitioned plan (fills val_off / rec_bytes from val_slots)
+void jit_layout_records(JitPlan* p);
+// LDS bytes of the scatter pass for a staging capacity
+size_t jit_scatter_lds(const JitPlan& p, int cap);
 struct JitKernel {
   std::vector<char> image;
   hipModule_t module = nullptr;

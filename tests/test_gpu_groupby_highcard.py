@@ -57,8 +57,15 @@ def test_highcard_partitioned_vs_oracle(engine, qi, n, monkeypatch):
     assert_same_groups(res.groups(), og, _fsum(qc))
 
 
-def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch):
-    """Same query through the partitioned plan and the direct HBM-atomic plan: identical groups."""
+@pytest.mark.parametrize("stage_cap", [None, "0", "4"])
+def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch, stage_cap):
+    """Same query through the partitioned plan and the direct HBM-atomic plan: identical groups.
+    stage_cap: scatter records staged per partition in LDS (None: planner's choice; 0: direct
+    writes; 4: tiny staging, most records take the overflow path)."""
+    if stage_cap is None:
+        monkeypatch.delenv("PINOT_AMD_STAGE_CAP", raising=False)
+    else:
+        monkeypatch.setenv("PINOT_AMD_STAGE_CAP", stage_cap)
     rng = np.random.default_rng(77)
     bufs = [random_segment(rng, 200_000 + 999 * i, name=f"s{i}", bits_cards=(1000, 700)) for i in range(3)]
     segs = [engine.ImmutableSegment(b) for b in bufs]

@@ -337,3 +337,31 @@ def test_lz4_raw_columns_staged(engine, comp, kernel_mode):
     nm, og = oracle.execute(q, [bufs])
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3, 4, 5, 7, 8, 9, 11, 13, 15, 16, 17])
+@pytest.mark.parametrize("generic", [False, True])
+def test_fixed_bit_widths_through_scan(engine, bits, generic, monkeypatch):
+    """Every dictionary bit width through the fused scan: widths <= 15 shared by the batch decode
+    with compile-time shifts (fixed_bit4_c), others (or PINOT_AMD_GENERIC_BITS=1) generically."""
+    monkeypatch.setenv("PINOT_AMD_JIT", "1")
+    monkeypatch.setenv("PINOT_AMD_GENERIC_BITS", "1" if generic else "0")
+    rng = np.random.default_rng(bits)
+    card = (1 << (bits - 1)) + 1 if bits > 1 else 2
+    n = max(40_003, card + 1000)
+    bufs = []
+    for i in range(2):
+        vals = rng.integers(0, card, n)
+        vals[:card] = np.arange(card)
+        cols = {"c": ((vals * 3 + 1).astype(np.int32), S.INT, {}),
+                "m": (rng.integers(-1000, 1000, n).astype(np.int32), S.INT, {"dictionary": False})}
+        bufs.append(S.build_segment(f"b{bits}_{i}", cols))
+    assert bufs[0].columns["c"].bits_per_element == bits
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    hi = 3 * (card // 2) + 1
+    q = f"SELECT c, COUNT(*), SUM(m), MIN(m) FROM t WHERE c <= {hi} GROUP BY c OPTION(numGroupsLimit=1000000)"
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert res.kernel_info().startswith("jit")
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
