@@ -1,6 +1,6 @@
 """Benchmark: rows scanned/s + achieved HBM GB/s of a filter + group-by query (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], 1B rows in 100 segments per GPU): each rank holds
+Default workload (BASELINE.json configs[1], 1B rows in 100 segments per GPU): each rank holds
 --segments immutable segments of --rows rows of the AdAnalytics-style table in HBM
 (pinot_amd/datagen.py: two fixed-bit dictionary-encoded columns, raw INT/LONG/DOUBLE metrics) and
 runs the filter + group-by query pinot_amd.datagen.BENCH_QUERY over all of them. A step is one full
@@ -8,7 +8,11 @@ execution of that query over the rank's segments (one batched scan kernel over 1
 N > 1, the RCCL all-reduce of the dense group tables. Segments are independent, so per-GPU work is
 fixed as N grows (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Other workloads (one JSON line per query; not the driver's headline line):
+  --workload highcard   configs[3]: GROUP BY two 1000-value dimensions (1M groups), partitioned plan
+  --workload inverted   configs[2]: inverted-index IN filters, AND/OR over 3 columns, selectivity sweep
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload scan|highcard|inverted]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -23,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+METRIC = "rows scanned/sec + achieved HBM GB/s, filter+group-by query, 1/2/4/8 GPUs"
 
 
 def log(*a):
@@ -30,24 +35,28 @@ def log(*a):
 
 
 def workloads():
-    """name -> (segment generator, query, algorithmic HBM bytes per row, description)."""
+    """name -> (segment generator, [queries], algorithmic HBM bytes per row, description, distinct segments)."""
     from pinot_amd import datagen
     return {
-        "scan": (datagen.ad_segment, datagen.BENCH_QUERY, datagen.BENCH_BYTES_PER_ROW,
+        "scan": (datagen.ad_segment, [datagen.BENCH_QUERY], datagen.BENCH_BYTES_PER_ROW,
                  "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE columns; "
-                 "filter+group-by query"),
-        "highcard": (datagen.highcard_segment, datagen.HIGHCARD_QUERY, datagen.HIGHCARD_BYTES_PER_ROW,
+                 "filter+group-by query", None),
+        "highcard": (datagen.highcard_segment, [datagen.HIGHCARD_QUERY], datagen.HIGHCARD_BYTES_PER_ROW,
                      "configs[3]: high-cardinality GROUP BY on 2 dims (1M groups), SUM/COUNT/MIN/MAX, "
-                     "100 segments x 10M rows per GPU (8B rows on 8 GPUs), RCCL merge of the group tables"),
+                     "100 segments x 10M rows per GPU (8B rows on 8 GPUs), RCCL merge of the group tables", None),
+        "inverted": (datagen.inverted_segment, [datagen.inverted_query(s) for s in datagen.INVERTED_SELECTIVITIES],
+                     None,
+                     "configs[2]: inverted-index IN filters combined with AND/OR across 3 columns (10000-value "
+                     "dictionaries, RoaringBitmap inverted indexes), selectivity sweep, 1B rows on 1 GPU", 4),
     }
 
 
-def cpu_baseline(workload: str, seg_rows: int, seconds: float):
+def cpu_baseline(workload: str, query: str, seg_rows: int, seconds: float):
     """Time the CPU oracle (scalar C port of the reference path, 1 core) on freshly generated
     segments of the same workload until `seconds` of CPU work have run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    gen, query, _, _ = workloads()[workload]
+    gen = workloads()[workload][0]
     rows = 0
     t_cpu = 0.0
     k = 0
@@ -63,10 +72,26 @@ def cpu_baseline(workload: str, seg_rows: int, seconds: float):
                       f"(scalar restatement of the reference Java path), {t_cpu:.1f} s"}
 
 
+def query_bytes_per_row(query: str, seg) -> float:
+    """Algorithmic HBM bytes per row: every column the query references, read once (fixed-bit
+    columns at their bit width, raw columns at their value width)."""
+    from pinot_amd.query import parse_sql
+    from pinot_amd.segment import VALUE_SIZE
+    qc = parse_sql(query)
+    cols = set(qc.group_by) | {a.column for a in qc.aggregations if a.column != "*"}
+    for clause in qc.cnf:
+        cols |= {p.column for p, _ in clause}
+    total = 0.0
+    for c in cols:
+        cb = seg.columns[c]
+        total += cb.bits_per_element / 8.0 if cb.has_dictionary else VALUE_SIZE[cb.stored_type]
+    return total
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="scan", choices=["scan", "highcard"])
+    ap.add_argument("--workload", default="scan", choices=["scan", "highcard", "inverted"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segments", type=int, default=100)
@@ -78,9 +103,9 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from pinot_amd import datagen, dist as pdist, engine
+    from pinot_amd import dist as pdist, engine
     from pinot_amd.query import parse_sql
-    gen, query, bytes_per_row, workload_desc = workloads()[args.workload]
+    gen, queries, bytes_per_row, workload_desc, distinct = workloads()[args.workload]
 
     rank, world, local = pdist.init_distributed()
     torch.cuda.set_device(local)
@@ -90,143 +115,160 @@ def main():
     # ---- stage this rank's segments into HBM ----
     t0 = time.time()
     segs = []
+    host_bufs = []
     for i in range(args.segments):
-        bufs = gen(f"{args.workload}_{rank}_{i}", args.rows, seed=rank * 100_003 + i)
+        if distinct is None or i < distinct:
+            bufs = gen(f"{args.workload}_{rank}_{i}", args.rows, seed=rank * 100_003 + i)
+            if distinct is not None:
+                host_bufs.append(bufs)
+        else:  # slow-to-build workloads: further segments are HBM copies of the first `distinct`
+            bufs = host_bufs[i % distinct]
         segs.append(engine.ImmutableSegment(bufs))
-        del bufs
+        if i == 0:
+            first_bufs = bufs
         if i % 20 == 19:
             log(f"[rank {rank}] staged {i + 1}/{args.segments} segments ({time.time() - t0:.0f}s)")
     hbm = sum(s.device_bytes() for s in segs)
     log(f"[rank {rank}] {args.segments} segments, {hbm / 1e9:.1f} GB in HBM, staged in {time.time() - t0:.0f}s")
+    data = "synthetic (device-generated segments in Pinot's on-disk formats)"
+    if distinct is not None:
+        data += f"; {distinct} distinct segments, each staged {args.segments // distinct}x"
 
     stream = torch.cuda.current_stream()
     ex = engine.ServerQueryExecutor()
-    res = ex.execute(query, segs, stream=stream)
-    scratch = None
-
-    def step():
-        nonlocal scratch
-        res.execute_again(stream)
-        if world > 1:
-            scratch = pdist.merge_result(res, scratch, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    kernel_ms = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        kernel_ms.append(res.last_kernel_ms())  # HIP events around the scan kernel on `stream`
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
     rows_per_rank = args.segments * args.rows
-    total_rows = rows_per_rank * world * args.steps
-    value = total_rows / elapsed
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    alg_bytes = rows_per_rank * bytes_per_row   # per launch (one launch = all segments)
-    achieved = alg_bytes / avg_kernel_s / 1e9
+    outs = []
+    for query in queries:
+        bpr = bytes_per_row if bytes_per_row is not None else query_bytes_per_row(query, first_bufs)
+        res = ex.execute(query, segs, stream=stream)
+        scratch = None
 
-    groups = res.groups()
-    matched = res.num_docs_matched()
-    if world > 1:
-        m = torch.tensor([matched], dtype=torch.int64, device="cuda")
-        dist.all_reduce(m)
-        matched_all = int(m.item())
-    else:
-        matched_all = matched
-    # size-independent property: the merged group COUNTs add up to the docs that passed the filter
-    assert sum(p[0] for p in groups.values()) == matched_all, "sum of group COUNTs != matched docs"
+        def step():
+            nonlocal scratch
+            res.execute_again(stream)
+            if world > 1:
+                scratch = pdist.merge_result(res, scratch, stream=stream)
 
-    if args.check and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        one = gen("check", min(args.rows, 2_000_000), seed=424242)
-        r1 = ex.execute(query, [engine.ImmutableSegment(one)]).groups()
-        _, o1 = oracle.execute(query, [one])
-        assert set(r1) == set(o1), "group keys differ"
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+
+        kernel_ms = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            kernel_ms.append(res.last_kernel_ms())  # HIP events around the device plan on `stream`
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+
+        total_rows = rows_per_rank * world * args.steps
+        value = total_rows / elapsed
+        avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        alg_bytes = rows_per_rank * bpr   # per launch (one launch = all segments)
+        achieved = alg_bytes / avg_kernel_s / 1e9
+
+        groups = res.groups()
+        matched = res.num_docs_matched()
+        if world > 1:
+            m = torch.tensor([matched], dtype=torch.int64, device="cuda")
+            dist.all_reduce(m)
+            matched_all = int(m.item())
+        else:
+            matched_all = matched
         qc = parse_sql(query)
-        for k in o1:
-            for i, a in enumerate(qc.aggregations):
-                g, e = r1[k][i], o1[k][i]
-                if a.func == "SUM" and isinstance(e, float) and e != int(e):
-                    assert abs(g - e) <= 1e-12 * abs(e), (k, a.name, g, e)
-                else:
-                    assert g == e, (k, a.name, g, e)
-        log("[check] HIP result == oracle on a 2M-row segment")
+        # size-independent property: the merged group COUNTs add up to the docs that passed the filter
+        if qc.group_by:
+            assert sum(p[0] for p in groups.values()) == matched_all, "sum of group COUNTs != matched docs"
+        elif world == 1 and qc.aggregations and qc.aggregations[0].func == "COUNT":
+            assert groups[()][0] == matched, "COUNT(*) != matched docs"
 
-    # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
-    # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
-    traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_summary_bench40seg.json")
-    if os.path.exists(pmc) and res.kernel_info() == "jit" and args.workload == "scan":
-        d = json.load(open(pmc))["derived"]
-        traffic = (d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]) / d["rows_per_launch"] * rows_per_rank
-        traffic_src = "profiles/r01/pmc_summary_bench40seg.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-row)"
+        if args.check and rank == 0:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            one = gen("check", min(args.rows, 2_000_000), seed=424242)
+            r1 = ex.execute(query, [engine.ImmutableSegment(one)]).groups()
+            _, o1 = oracle.execute(query, [one])
+            assert set(r1) == set(o1), "group keys differ"
+            for k in o1:
+                for i, a in enumerate(qc.aggregations):
+                    g, e = r1[k][i], o1[k][i]
+                    if a.func == "SUM" and isinstance(e, float) and e != int(e):
+                        assert abs(g - e) <= 1e-12 * abs(e), (k, a.name, g, e)
+                    else:
+                        assert g == e, (k, a.name, g, e)
+            log("[check] HIP result == oracle on a 2M-row segment")
 
-    out = None
-    if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            log("[rank 0] timing the CPU baseline ...")
-            cpu = cpu_baseline(args.workload, min(args.rows, 10_000_000), args.cpu_seconds)
-        out = {
-            "metric": "rows scanned/sec + achieved HBM GB/s, filter+group-by query, 1/2/4/8 GPUs",
-            "value": value,
-            "unit": "rows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int32/int64/f64",
-            "data": "synthetic (device-generated segments in Pinot's on-disk formats)",
-            "config": {
-                "workload": workload_desc,
-                "query": query,
-                "segments_per_gpu": args.segments,
-                "rows_per_segment": args.rows,
-                "rows_per_gpu": rows_per_rank,
-                "selectivity": matched / rows_per_rank,
-                "groups": len(groups),
-                "parallelism": f"segments sharded over {world} GPU(s), RCCL all-reduce merge" if world > 1
-                               else "1 GPU",
-                "hbm_bytes_per_gpu": hbm,
-                "scan_kernel": res.kernel_info(),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel": {"jit": "pinot_scan_jit", "jit-partitioned": "pinot_part_count+scatter+agg"}.get(
-                    res.kernel_info(), "pamd::scan_kernel<4,true,false>"),
-                "kernel_ms": avg_kernel_s * 1e3,
-                "bytes_per_row": bytes_per_row,
-            },
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
+        # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
+        # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
+        traffic, traffic_src = None, None
+        pmc = os.path.join(ROOT, "profiles", "r01", "pmc_summary_bench40seg.json")
+        if os.path.exists(pmc) and res.kernel_info() == "jit" and args.workload == "scan":
+            d = json.load(open(pmc))["derived"]
+            traffic = (d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]) / d["rows_per_launch"] * rows_per_rank
+            traffic_src = "profiles/r01/pmc_summary_bench40seg.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-row)"
+
+        if rank == 0:
+            cpu = None
+            if not args.no_cpu_baseline and world == 1:
+                log("[rank 0] timing the CPU baseline ...")
+                cpu = cpu_baseline(args.workload, query, min(args.rows, 10_000_000), args.cpu_seconds)
+            out = {
+                "metric": METRIC,
+                "value": value,
+                "unit": "rows/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "int32/int64/f64",
+                "data": data,
+                "config": {
+                    "workload": workload_desc,
+                    "query": query if len(query) < 400 else query[:200] + " ... " + query[-120:],
+                    "segments_per_gpu": args.segments,
+                    "rows_per_segment": args.rows,
+                    "rows_per_gpu": rows_per_rank,
+                    "selectivity": matched / rows_per_rank,
+                    "groups": len(groups),
+                    "parallelism": f"segments sharded over {world} GPU(s), RCCL all-reduce merge" if world > 1
+                                   else "1 GPU",
+                    "hbm_bytes_per_gpu": hbm,
+                    "scan_kernel": res.kernel_info(),
+                },
+                "roofline": {
+                    "bound": "hbm",
+                    "achieved": achieved,
+                    "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": traffic,
+                    "traffic_source": traffic_src,
+                    "kernel": {"jit": "pinot_scan_jit", "jit-partitioned": "pinot_part_count+scatter+agg"}.get(
+                        res.kernel_info(), "pamd::scan_kernel<4,true,false>"),
+                    "kernel_ms": avg_kernel_s * 1e3,
+                    "bytes_per_row": bpr,
+                },
+                "cpu_baseline": cpu,
+            }
+            print(json.dumps(out), flush=True)
+            outs.append(out)
+        res.destroy()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return out
+    return outs[0] if len(outs) == 1 else outs
 
 
 if __name__ == "__main__":

@@ -80,6 +80,20 @@ struct DevPartition {
   uint8_t* rec;
 };
 
+// Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the
+// predicate selects) are OR-ed into a dense docId bitset (BitmapBasedFilterOperator's bitmap OR).
+struct ExpandJob {
+  const uint8_t* inv;          // staged inverted-index buffer
+  const struct RoaringContainer* conts;  // container directory of the column
+  const int32_t* sel;          // selected container indices, grouped by 65536-doc chunk
+  const int32_t* grp;          // chunk k's containers: sel[grp[k] .. grp[k+1])
+  unsigned long long* bitset;  // output, nwords 64-bit words (every word written each run)
+  int64_t num_docs, nwords;
+  int64_t sel_begin;           // prefix of nsel over the plan's jobs
+  int64_t item_begin;          // prefix of nchunks over the plan's jobs (work items)
+  int32_t nsel, nchunks;
+};
+
 // Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the
 // kernel's per-slot loop indexes the decoded values with compile-time indices only.
 struct DevQuery {

@@ -37,8 +37,7 @@ hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* 
                                hipStream_t st);
 hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
                                  int32_t* out, hipStream_t st);
-hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const int32_t* sel, int32_t nsel,
-                                 int64_t num_docs, uint64_t* bitset, hipStream_t st);
+hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
 hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
                                     int64_t* d_part_begin, hipStream_t st);
 }  // namespace pamd
@@ -190,6 +189,8 @@ struct Column {
   DevBuf inv;
   DevBuf inv_conts;
   std::vector<uint32_t> inv_dir;  // containers of dictId d: [inv_dir[d], inv_dir[d+1])
+  std::vector<uint64_t> inv_bytes;  // serialized bitmap bytes of dictIds < d (prefix, card+1 entries)
+  std::vector<uint16_t> inv_keys;   // container -> key (high 16 bits of its docIds)
   bool has_inv = false;
 };
 
@@ -252,6 +253,7 @@ static int decode_dictionary(Column& c, const uint8_t* d, size_t n) {
 static int build_inverted_directory(Column& c, const uint8_t* inv, size_t n) {
   std::vector<RoaringContainerHost> conts;
   c.inv_dir.assign(1, 0);
+  c.inv_bytes.assign(1, 0);
   const size_t hdr = 4 * ((size_t)c.card + 1);
   if (n < hdr) return fail(PINOT_AMD_EINVAL, "inverted index too small");
   const uint32_t first = be32(inv);
@@ -303,8 +305,10 @@ static int build_inverted_directory(Column& c, const uint8_t* inv, size_t n) {
       }
       if (pos > len) return fail(PINOT_AMD_EINVAL, "truncated bitmap %d", d);
       conts.push_back(rc);
+      c.inv_keys.push_back((uint16_t)rc.key);
     }
     c.inv_dir.push_back((uint32_t)conts.size());
+    c.inv_bytes.push_back((c.inv_bytes.empty() ? 0 : c.inv_bytes.back()) + len);
   }
   int rc = c.inv.alloc_copy(inv, n, 64);
   if (rc) return rc;
@@ -665,11 +669,14 @@ struct pinot_amd_result {
     int seg;
     const Column* col;
     DevBuf* bitset;
-    DevBuf* sel;
-    int32_t nsel;
+    DevBuf* sel;   // selected container indices grouped by chunk
+    DevBuf* grp;   // chunk k's containers: sel[grp[k] .. grp[k+1])
+    int32_t nsel, nchunks;
     int64_t num_docs;
   };
   std::vector<InvLeaf> inv_leaves;
+  DevBuf d_expand_jobs;        // one ExpandJob per inv_leaves entry (batched clear + expand launches)
+  int64_t expand_total = 0;   // work items: (job, 65536-doc chunk) pairs
   int grid = 1;
   std::vector<std::unique_ptr<DevBuf>> bitsets;  // filter-only plans: one docId bitset per segment
   std::vector<int64_t> bitset_words;
@@ -788,8 +795,36 @@ static void dict_range_of(const PredSpec& p, const Column& c, int64_t* start, in
 
 }  // namespace
 
+// Evaluate an EQ/IN/RANGE predicate through the bitmap inverted index or through the forward
+// index? Both give the same docId set; pick the one that moves fewer bytes: the selected bitmaps
+// (serialized size, ~its container payloads) plus writing and re-reading the dense bitset, against
+// decoding the fixed-bit forward index (free when the column is decoded anyway for GROUP BY /
+// aggregation). PINOT_AMD_INV_POLICY=always|never overrides (tests).
+static bool use_inverted_for(const Column& c, int64_t num_docs, const std::vector<int32_t>& ids, bool is_range,
+                             int64_t start, int64_t end, bool decoded_anyway) {
+  if (const char* pol = getenv("PINOT_AMD_INV_POLICY")) {
+    if (strcmp(pol, "always") == 0) return true;
+    if (strcmp(pol, "never") == 0) return false;
+  }
+  uint64_t inv = 0;
+  int64_t nconts = 0;
+  if (is_range) {
+    inv = c.inv_bytes[end] - c.inv_bytes[start];
+    nconts = (int64_t)c.inv_dir[end] - c.inv_dir[start];
+  } else {
+    for (int32_t d : ids) {
+      inv += c.inv_bytes[d + 1] - c.inv_bytes[d];
+      nconts += (int64_t)c.inv_dir[d + 1] - c.inv_dir[d];
+    }
+  }
+  const double inv_cost = (double)inv + 64.0 * (double)nconts + 2.0 * (double)num_docs / 8.0;
+  const double scan_cost = decoded_anyway ? 0.0 : (double)num_docs * c.bits / 8.0;
+  return inv_cost < scan_cost;
+}
+
 static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_segment* seg, const PredSpec& p,
-                                 const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st) {
+                                 const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
+                                 bool decoded_anyway) {
   memset(L, 0, sizeof(*L));
   L->slot = slot;
   L->clause = p.clause;
@@ -901,23 +936,41 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     *needs_slot = false;
     return 0;
   }
-  if (p.use_inv && c.has_inv) {
+  if (p.use_inv && c.has_inv && c.enc == ENC_FIXED_BIT &&
+      use_inverted_for(c, seg->num_docs, ids, is_range, start, end, decoded_anyway)) {
     // BitmapBasedFilterOperator: OR of the inverted-index bitmaps of the matching dictIds
     if (is_range) {
       ids.clear();
       for (int64_t d = start; d < end; ++d) ids.push_back((int32_t)d);
     }
-    std::vector<int32_t> sel;
-    for (int32_t d : ids)
-      for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k) sel.push_back((int32_t)k);
+    // selected containers grouped by 65536-doc chunk (container key): the expansion builds each
+    // chunk of the dense bitset in LDS from its group and writes it out once
     const int64_t tiles = (seg->num_docs + kTileDocs - 1) / kTileDocs;
+    const size_t bs_bytes = (size_t)std::max<int64_t>(tiles, 1) * kTileDocs / 8 + 64;
+    const int32_t nchunks = (int32_t)((bs_bytes / 8 + 1023) / 1024);
+    std::vector<int32_t> grp(nchunks + 1, 0);
+    for (int32_t d : ids)
+      for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k)
+        if (c.inv_keys[k] < nchunks) ++grp[c.inv_keys[k] + 1];
+    for (int32_t k = 0; k < nchunks; ++k) grp[k + 1] += grp[k];
+    std::vector<int32_t> sel(grp[nchunks]);
+    {
+      std::vector<int32_t> fillp(grp.begin(), grp.end() - 1);
+      for (int32_t d : ids)
+        for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k)
+          if (c.inv_keys[k] < nchunks) sel[fillp[c.inv_keys[k]]++] = (int32_t)k;
+    }
     auto bs = std::make_unique<DevBuf>();
-    int rc = bs->alloc((size_t)std::max<int64_t>(tiles, 1) * kTileDocs / 8 + 64);
+    int rc = bs->alloc(bs_bytes);
     if (rc) return rc;
     auto sb = std::make_unique<DevBuf>();
     rc = sb->alloc_copy(sel.data(), sel.size() * 4, 64);
     if (rc) return rc;
-    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), (int32_t)sel.size(), seg->num_docs});
+    auto gb = std::make_unique<DevBuf>();
+    rc = gb->alloc_copy(grp.data(), grp.size() * 4, 64);
+    if (rc) return rc;
+    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), nchunks, seg->num_docs});
+    r->owned.push_back(std::move(gb));
     L->kind = LEAF_DOC_BITSET;
     L->bits = (const uint32_t*)bs->p;
     L->slot = -1;
@@ -985,14 +1038,11 @@ static int remap_for(const Column& c, const MergedKeyColumn& m, std::vector<int3
 static int run_plan(pinot_amd_result* r) {
   hipStream_t st = r->stream;
   // inverted-index leaves: expand roaring containers into dense doc bitsets
-  for (auto& il : r->inv_leaves) {
-    HIP_OK(hipMemsetAsync(il.bitset->p, 0, il.bitset->n, st));
-    HIP_OK(launch_roaring_expand((const uint8_t*)il.col->inv.p, il.col->inv_conts.p, (const int32_t*)il.sel->p,
-                                 il.nsel, il.num_docs, (uint64_t*)il.bitset->p, st));
-  }
+  HIP_OK(hipEventRecord(r->ev0, st));
+  if (!r->inv_leaves.empty())
+    HIP_OK(launch_expand_jobs(r->d_expand_jobs.p, (int32_t)r->inv_leaves.size(), r->expand_total, st));
   HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
   if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
-  HIP_OK(hipEventRecord(r->ev0, st));
   if (r->jit && r->partitioned) {
     const DevSegment* segs = (const DevSegment*)r->d_segs.p;
     uint64_t* acc = (uint64_t*)r->acc.p;
@@ -1080,7 +1130,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const PredSpec& p = Q.preds[pi];
       const Column& c = *segs[si]->cols.at(p.column);
       bool needs_slot = false;
-      int rc = make_leaf_for_segment(r, si, segs[si], p, c, -1, &seg_leaves[si][pi], &needs_slot, r->stream);
+      bool decoded_anyway = std::find(Q.group_by.begin(), Q.group_by.end(), p.column) != Q.group_by.end();
+      for (auto& a : Q.aggs) decoded_anyway |= a.column == p.column;
+      int rc = make_leaf_for_segment(r, si, segs[si], p, c, -1, &seg_leaves[si][pi], &needs_slot, r->stream,
+                                     decoded_anyway);
       if (rc) return rc;
       if (needs_slot) leaf_slot_col[si][pi] = slot_of(p.column);
     }
@@ -1242,6 +1295,31 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
 
   int rc = r->d_segs.alloc_copy(r->hsegs.data(), r->hsegs.size() * sizeof(DevSegment), 0);
   if (rc) return rc;
+  if (!r->inv_leaves.empty()) {
+    std::vector<ExpandJob> jobs(r->inv_leaves.size());
+    int64_t total = 0, items = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      const auto& il = r->inv_leaves[j];
+      ExpandJob& J = jobs[j];
+      memset(&J, 0, sizeof(J));
+      J.inv = (const uint8_t*)il.col->inv.p;
+      J.conts = (const RoaringContainer*)il.col->inv_conts.p;
+      J.sel = (const int32_t*)il.sel->p;
+      J.bitset = (unsigned long long*)il.bitset->p;
+      J.num_docs = il.num_docs;
+      J.nwords = (int64_t)(il.bitset->n / 8);
+      J.sel_begin = total;
+      J.nsel = il.nsel;
+      J.grp = (const int32_t*)il.grp->p;
+      J.item_begin = items;
+      J.nchunks = il.nchunks;
+      total += il.nsel;
+      items += il.nchunks;
+    }
+    r->expand_total = items;
+    rc = r->d_expand_jobs.alloc_copy(jobs.data(), jobs.size() * sizeof(ExpandJob), 0);
+    if (rc) return rc;
+  }
   if (filter_only) {
     std::vector<uint64_t*> ptrs;
     for (int si = 0; si < n; ++si) {

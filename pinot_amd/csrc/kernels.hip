@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "device_types.h"
 
 namespace pamd {
@@ -696,32 +698,90 @@ struct RoaringContainer {
   uint64_t offset;   // byte offset of the container payload inside the staged inverted index
 };
 
-__global__ void roaring_expand_kernel(const uint8_t* inv, const RoaringContainer* conts, const int32_t* sel,
-                                      int64_t num_docs, unsigned long long* bitset) {
-  const RoaringContainer c = conts[sel[blockIdx.x]];
-  const uint8_t* p = inv + c.offset;
-  const int64_t base = (int64_t)c.key << 16;
-  if (c.kind == 1) {
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-      const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
-      const int64_t d = base + 64 * i;
-      if (w && d < num_docs) atomicOr(&bitset[d >> 6], (unsigned long long)w);
+// Batched expansion: every (segment, inverted-index leaf) of a plan is one ExpandJob; a work item
+// is one 65536-doc chunk of one job. A block builds its chunk's 8 KiB of bitset in LDS from the
+// chunk's selected containers (LDS atomics, no global atomics), then writes all 1024 words once
+// (chunks with no container write zeros, so no separate clear pass). Small array containers are
+// expanded one per lane; bitmap, run and large array containers by a whole wave.
+__global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const ExpandJob* jobs, int32_t njobs,
+                                                                      int64_t total_items) {
+  __shared__ uint32_t lbits[2048];
+  __shared__ int32_t bigq[kBlock];
+  __shared__ int32_t nbig;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].item_begin <= item) lo = mid; else hi = mid - 1;
     }
-  } else if (c.kind == 0) {
-    for (uint32_t i = threadIdx.x; i < c.count; i += blockDim.x) {
-      const int64_t d = base + (p[2 * i] | (p[2 * i + 1] << 8));
-      if (d < num_docs) atomicOr(&bitset[d >> 6], 1ull << (d & 63));
+    const ExpandJob& J = jobs[lo];
+    const int32_t k = (int32_t)(item - J.item_begin);
+    for (int i = tid; i < 2048; i += kBlock) lbits[i] = 0u;
+    if (tid == 0) nbig = 0;
+    __syncthreads();
+    const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
+    for (int32_t base = g0; base < g1; base += kBlock) {
+      const int32_t ci = base + tid;
+      if (ci < g1) {
+        const RoaringContainer c = J.conts[J.sel[ci]];
+        const uint8_t* p = J.inv + c.offset;
+        if (c.kind == 0 && c.count <= 16) {
+          for (uint32_t e = 0; e < c.count; ++e) {
+            const uint32_t d = p[2 * e] | (p[2 * e + 1] << 8);
+            atomicOr(&lbits[d >> 5], 1u << (d & 31));
+          }
+        } else {
+          bigq[atomicAdd(&nbig, 1)] = J.sel[ci];
+        }
+      }
+      __syncthreads();
+      const int nb = nbig;
+      for (int qi = wave; qi < nb; qi += kBlock / 64) {
+        const RoaringContainer c = J.conts[bigq[qi]];
+        const uint8_t* p = J.inv + c.offset;
+        if (c.kind == 1) {
+          for (int i = lane; i < 1024; i += 64) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
+            if (w) {
+              atomicOr(&lbits[2 * i], (uint32_t)w);
+              atomicOr(&lbits[2 * i + 1], (uint32_t)(w >> 32));
+            }
+          }
+        } else if (c.kind == 0) {
+          for (uint32_t e = lane; e < c.count; e += 64) {
+            const uint32_t d = p[2 * e] | (p[2 * e + 1] << 8);
+            atomicOr(&lbits[d >> 5], 1u << (d & 31));
+          }
+        } else {
+          for (uint32_t r = 0; r < c.count; ++r) {
+            const uint8_t* q = p + 2 + 4 * r;
+            const uint32_t s0 = q[0] | (q[1] << 8);
+            const uint32_t e0 = s0 + (q[2] | (q[3] << 8));  // inclusive, < 65536
+            const uint32_t w0 = s0 >> 5, w1 = e0 >> 5;
+            for (uint32_t w = w0 + lane; w <= w1; w += 64) {
+              uint32_t m = ~0u;
+              if (w == w0) m &= ~0u << (s0 & 31);
+              if (w == w1) m &= ~0u >> (31 - (e0 & 31));
+              atomicOr(&lbits[w], m);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0) nbig = 0;
+      __syncthreads();
     }
-  } else {
-    for (uint32_t r = 0; r < c.count; ++r) {
-      const uint8_t* q = p + 2 + 4 * r;
-      const int64_t s = base + (q[0] | (q[1] << 8));
-      const int64_t l = q[2] | (q[3] << 8);
-      for (int64_t d = s + threadIdx.x; d <= s + l; d += blockDim.x)
-        if (d < num_docs) atomicOr(&bitset[d >> 6], 1ull << (d & 63));
+    // write the chunk (docs >= num_docs are never set: bitmaps hold only the segment's docIds)
+    const int64_t w_begin = (int64_t)k * 1024;
+    for (int i = tid; i < 1024; i += kBlock) {
+      const int64_t w = w_begin + i;
+      if (w < J.nwords) J.bitset[w] = (unsigned long long)lbits[2 * i] | ((unsigned long long)lbits[2 * i + 1] << 32);
     }
+    __syncthreads();
   }
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // launchers (called from host.cpp)
@@ -840,14 +900,6 @@ hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const i
   return hipGetLastError();
 }
 
-hipError_t launch_roaring_expand(const uint8_t* inv, const void* conts, const int32_t* sel, int32_t nsel,
-                                 int64_t num_docs, uint64_t* bitset, hipStream_t st) {
-  if (nsel <= 0) return hipSuccess;
-  hipLaunchKernelGGL(roaring_expand_kernel, dim3((unsigned)nsel), dim3(kBlock), 0, st, inv,
-                     reinterpret_cast<const RoaringContainer*>(conts), sel, num_docs,
-                     reinterpret_cast<unsigned long long*>(bitset));
-  return hipGetLastError();
-}
 
 hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
                                     int64_t* d_part_begin, hipStream_t st) {
@@ -856,6 +908,15 @@ hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int6
                      d_part_begin);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, d_part_begin, (int64_t)nparts,
                      d_part_begin + nparts);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st) {
+  if (njobs <= 0 || total_items <= 0) return hipSuccess;
+  const ExpandJob* jobs = reinterpret_cast<const ExpandJob*>(d_jobs);
+  const int64_t blocks = std::min<int64_t>(total_items, 16384);
+  hipLaunchKernelGGL(roaring_expand_chunks_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs,
+                     total_items);
   return hipGetLastError();
 }
 

@@ -106,3 +106,62 @@ def highcard_segment(name: str, num_docs: int, seed: int, device: str = "cuda") 
 HIGHCARD_QUERY = ("SET numGroupsLimit = 2000000; SELECT dimA, dimB, COUNT(*), SUM(metInt), MIN(metLong), "
                   "MAX(metDouble) FROM highCard WHERE metInt < 900 GROUP BY dimA, dimB")
 HIGHCARD_BYTES_PER_ROW = 2 * S.num_bits_per_value(HC_CARD - 1) / 8.0 + 4 + 8 + 8
+
+
+# ---------------------------------------------------------------------------------------------
+# BASELINE.json configs[2]: inverted-index EQ/IN filters combined with AND/OR across 3 columns
+INV_CARD = 10000           # dictionary cardinality of invA / invB / invC (14-bit fixed-bit forward index)
+INV_COLUMNS = ("invA", "invB", "invC")
+
+
+def inverted_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+    """Segment with three uniformly distributed dictionary-encoded INT columns carrying bitmap
+    inverted indexes (RoaringBitmap array containers, BitmapInvertedIndexWriter layout) and raw
+    INT / DOUBLE metrics."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = num_docs
+    cols = {}
+    bits = S.num_bits_per_value(INV_CARD - 1)
+    dvals = np.arange(INV_CARD, dtype=np.int32) * 3 + 1
+    for cname in INV_COLUMNS:
+        ids = torch.randint(0, INV_CARD, (n,), generator=g, device=device, dtype=torch.int32)
+        ids[:INV_CARD] = torch.arange(INV_CARD, device=device, dtype=torch.int32)
+        inv = S.inverted_index_bytes(ids.cpu().numpy(), INV_CARD)
+        cols[cname] = S.ColumnBuffers(cname, S.INT, n, True, False, INV_CARD, bits, _fixed_bit(ids, bits),
+                                      S.dictionary_bytes(dvals, S.INT), inv, dvals)
+    m = torch.randint(0, 1000, (n,), generator=g, device=device, dtype=torch.int32)
+    cost = torch.rand((n,), generator=g, device=device, dtype=torch.float64) * 100.0
+    cols["metInt"] = S.ColumnBuffers("metInt", S.INT, n, False, fwd=S.raw_fwd_header(n, S.INT) + _be_bytes(m, 4))
+    cols["cost"] = S.ColumnBuffers("cost", S.DOUBLE, n, False, fwd=S.raw_fwd_header(n, S.DOUBLE) + _be_bytes(cost, 8))
+    torch.cuda.synchronize()
+    return S.SegmentBuffers(name, n, cols)
+
+
+def inverted_fraction(selectivity: float) -> float:
+    """Per-column IN fraction f with f * (1 - (1 - f)^2) = selectivity (uniform independent columns)."""
+    lo, hi = 0.0, 1.0
+    for _ in range(60):
+        f = (lo + hi) / 2
+        if f * (2 * f - f * f) < selectivity:
+            lo = f
+        else:
+            hi = f
+    return (lo + hi) / 2
+
+
+def inverted_query(selectivity: float) -> str:
+    """invA IN (...) AND (invB IN (...) OR invC IN (...)), each IN list a fraction f of the
+    dictionary (values spread over it), for a target selectivity; COUNT + SUMs of raw metrics."""
+    f = inverted_fraction(selectivity)
+    k = max(1, int(round(f * INV_CARD)))
+    lists = []
+    for j in range(3):
+        ids = (np.arange(k, dtype=np.int64) * INV_CARD // k + j * 7) % INV_CARD
+        lists.append(", ".join(str(int(v) * 3 + 1) for v in np.unique(ids)))
+    return (f"SELECT COUNT(*), SUM(metInt), SUM(cost) FROM invTable WHERE invA IN ({lists[0]}) AND "
+            f"(invB IN ({lists[1]}) OR invC IN ({lists[2]}))")
+
+
+INVERTED_SELECTIVITIES = (0.0001, 0.001, 0.01, 0.1, 0.5)

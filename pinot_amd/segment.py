@@ -333,8 +333,69 @@ def roaring_serialize(doc_ids: np.ndarray, run_optimize: bool = True) -> bytes:
     return bytes(out)
 
 
+def _put_le(out: np.ndarray, pos: np.ndarray, val: np.ndarray, nbytes: int) -> None:
+    v = np.asarray(val, dtype=np.uint64)
+    for b in range(nbytes):
+        out[pos + b] = ((v >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8)
+
+
+def inverted_index_bytes_fast(dict_ids: np.ndarray, cardinality: int) -> Optional[bytes]:
+    """Vectorised ``inverted_index_bytes`` for the common case where every container of every
+    bitmap is an array container that runOptimize would keep (no bitmap or run containers): the
+    same bytes, built with numpy instead of one Python loop per container. Returns None when some
+    container needs another kind (the caller then uses the general builder)."""
+    d = np.asarray(dict_ids, dtype=np.int64)
+    n = d.size
+    card = int(cardinality)
+    hdr = 4 * (card + 1)
+    order = np.argsort(d, kind="stable")          # docIds ascending within each dictId
+    sd = d[order]
+    key = order >> 16
+    newc = np.ones(n, dtype=bool)
+    if n > 1:
+        newc[1:] = (sd[1:] != sd[:-1]) | (key[1:] != key[:-1])
+    cstart = np.nonzero(newc)[0]
+    ccard = np.diff(np.r_[cstart, n])
+    if n and int(ccard.max()) > ARRAY_MAX:
+        return None
+    brk = np.ones(n, dtype=bool)
+    if n > 1:
+        brk[1:] = newc[1:] | (order[1:] != order[:-1] + 1)
+    nruns = np.add.reduceat(brk.astype(np.int64), cstart) if n else np.zeros(0, np.int64)
+    if n and bool(((2 + 4 * nruns) < 2 * ccard).any()):   # runOptimize would pick a run container
+        return None
+    cdict = sd[cstart]
+    ckey = key[cstart]
+    nc_d = np.bincount(cdict, minlength=card).astype(np.int64)
+    nd_d = np.bincount(d, minlength=card).astype(np.int64)
+    size_d = 8 + 8 * nc_d + 2 * nd_d
+    bstart = hdr + np.r_[0, np.cumsum(size_d)[:-1]].astype(np.int64)
+    total = hdr + int(size_d.sum())
+    out = np.zeros(total, dtype=np.uint8)
+    out[:hdr] = np.r_[bstart, total].astype(">u4").view(np.uint8)
+    _put_le(out, bstart, np.full(card, ROARING_COOKIE_NO_RUN), 4)
+    _put_le(out, bstart + 4, nc_d, 4)
+    cfirst = np.r_[0, np.cumsum(nc_d)[:-1]]
+    dfirst = np.r_[0, np.cumsum(nd_d)[:-1]]
+    cj = np.arange(cstart.size) - cfirst[cdict]
+    cb = bstart[cdict]
+    _put_le(out, cb + 8 + 4 * cj, ckey, 2)
+    _put_le(out, cb + 10 + 4 * cj, ccard - 1, 2)
+    _put_le(out, cb + 8 + 4 * nc_d[cdict] + 4 * cj, 8 + 8 * nc_d[cdict] + 2 * (cstart - dfirst[cdict]), 4)
+    _put_le(out, bstart[sd] + 8 + 8 * nc_d[sd] + 2 * (np.arange(n) - dfirst[sd]), order & 0xFFFF, 2)
+    return out.tobytes()
+
+
 def inverted_index_bytes(dict_ids: np.ndarray, cardinality: int) -> bytes:
     """BitmapInvertedIndexWriter layout: (cardinality+1) BE absolute offsets, then bitmaps."""
+    fast = inverted_index_bytes_fast(dict_ids, cardinality)
+    if fast is not None:
+        return fast
+    return inverted_index_bytes_general(dict_ids, cardinality)
+
+
+def inverted_index_bytes_general(dict_ids: np.ndarray, cardinality: int) -> bytes:
+    """BitmapInvertedIndexWriter layout, any container kinds (one roaring_serialize per bitmap)."""
     d = np.asarray(dict_ids, dtype=np.int64)
     order = np.argsort(d, kind="stable")
     sd = d[order]

@@ -171,3 +171,17 @@ def test_lz4_known_block():
     blk = bytes([0x1F, ord("a"), 1, 0, 0x01, 0x50]) + b"bcdef"  # 'a' + match(off 1, len 4+15+1) + 'bcdef'
     n = oracle.lib().oracle_lz4_decompress(blk, len(blk), dst, 32)
     assert bytes(dst[:n]) == b"a" * 21 + b"bcdef"
+
+
+def test_vectorised_inverted_index_matches_general_builder():
+    """inverted_index_bytes_fast (numpy) == one roaring_serialize per bitmap, byte for byte, and
+    declines inputs that need bitmap or run containers."""
+    rng = np.random.default_rng(3)
+    for n, card in [(1, 1), (1000, 7), (100_000, 1000), (300_000, 50_000), (70_001, 9000)]:
+        ids = rng.integers(0, card, n)
+        ids[:min(card, n)] = np.arange(min(card, n))
+        fast = S.inverted_index_bytes_fast(ids, card)
+        assert fast is not None
+        assert fast == S.inverted_index_bytes_general(ids, card)
+    assert S.inverted_index_bytes_fast(rng.integers(0, 2, 70_000), 2) is None       # bitmap containers
+    assert S.inverted_index_bytes_fast(np.zeros(100, np.int64), 1) is None           # one run

@@ -30,6 +30,14 @@ def engine(torch_cuda):
     return E
 
 
+@pytest.fixture(autouse=True)
+def _inverted_index_always(monkeypatch):
+    """Predicates with use_inverted_index run through the bitmap inverted index whatever the cost
+    model would pick, so these tests keep exercising the roaring expansion (tests/test_gpu_inverted.py
+    covers the cost-based choice)."""
+    monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
+
+
 @pytest.fixture(params=["jit", "aot"])
 def kernel_mode(request, monkeypatch):
     """Run a test through the hipRTC query-specialised kernel and through the AOT generic kernel."""
