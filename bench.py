@@ -11,6 +11,7 @@ fixed as N grows (weak scaling).
 Other workloads (one JSON line per query; not the driver's headline line):
   --workload highcard   configs[3]: GROUP BY two 1000-value dimensions (1M groups), partitioned plan
   --workload inverted   configs[2]: inverted-index IN filters, AND/OR over 3 columns, selectivity sweep
+  --workload ssb        configs[4]: SSB SF100 denormalized lineorder, Q1.1-Q4.3
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload scan|highcard|inverted]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -36,7 +37,7 @@ def log(*a):
 
 def workloads():
     """name -> (segment generator, [queries], algorithmic HBM bytes per row, description, distinct segments)."""
-    from pinot_amd import datagen
+    from pinot_amd import datagen, ssb
     return {
         "scan": (datagen.ad_segment, [datagen.BENCH_QUERY], datagen.BENCH_BYTES_PER_ROW,
                  "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE columns; "
@@ -48,6 +49,9 @@ def workloads():
                      None,
                      "configs[2]: inverted-index IN filters combined with AND/OR across 3 columns (10000-value "
                      "dictionaries, RoaringBitmap inverted indexes), selectivity sweep, 1B rows on 1 GPU", 4),
+        "ssb": (ssb.lineorder_flat_segment, [sql for _, sql in ssb.SSB_QUERIES], None,
+                "configs[4]: Star Schema Benchmark SF100 denormalized lineorder (600M rows per GPU in 60 segments), "
+                "Q1.1-Q4.3 filter+group-by", None),
     }
 
 
@@ -78,7 +82,7 @@ def query_bytes_per_row(query: str, seg) -> float:
     from pinot_amd.query import parse_sql
     from pinot_amd.segment import VALUE_SIZE
     qc = parse_sql(query)
-    cols = set(qc.group_by) | {a.column for a in qc.aggregations if a.column != "*"}
+    cols = set(qc.group_by) | {c for a in qc.aggregations for c in a.columns}
     for clause in qc.cnf:
         cols |= {p.column for p, _ in clause}
     total = 0.0
@@ -91,10 +95,10 @@ def query_bytes_per_row(query: str, seg) -> float:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="scan", choices=["scan", "highcard", "inverted"])
+    ap.add_argument("--workload", default="scan", choices=["scan", "highcard", "inverted", "ssb"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--segments", type=int, default=100)
+    ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default 100; ssb: 60 = SF100)")
     ap.add_argument("--rows", type=int, default=10_000_000, help="rows per segment")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -106,6 +110,8 @@ def main():
     from pinot_amd import dist as pdist, engine
     from pinot_amd.query import parse_sql
     gen, queries, bytes_per_row, workload_desc, distinct = workloads()[args.workload]
+    if args.segments is None:
+        args.segments = 60 if args.workload == "ssb" else 100
 
     rank, world, local = pdist.init_distributed()
     torch.cuda.set_device(local)
@@ -186,9 +192,10 @@ def main():
             matched_all = matched
         qc = parse_sql(query)
         # size-independent property: the merged group COUNTs add up to the docs that passed the filter
-        if qc.group_by:
+        counts_first = bool(qc.aggregations) and qc.aggregations[0].func == "COUNT"
+        if qc.group_by and counts_first:
             assert sum(p[0] for p in groups.values()) == matched_all, "sum of group COUNTs != matched docs"
-        elif world == 1 and qc.aggregations and qc.aggregations[0].func == "COUNT":
+        elif world == 1 and counts_first:
             assert groups[()][0] == matched, "COUNT(*) != matched docs"
 
         if args.check and rank == 0:

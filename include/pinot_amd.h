@@ -174,6 +174,16 @@ int pinot_amd_query_add_predicate(pinot_amd_query* q, int32_t clause, const pino
 int pinot_amd_query_add_group_by(pinot_amd_query* q, const char* column);
 /* Aggregation function (column NULL or "*" for COUNT(*)). Returns the aggregation index via out_index. */
 int pinot_amd_query_add_aggregation(pinot_amd_query* q, int32_t agg_type, const char* column, int32_t* out_index);
+/* Aggregation over a binary arithmetic transform of two columns (SUM / MIN / MAX / AVG):
+ * MultiplicationTransformFunction (times), SubtractionTransformFunction (minus),
+ * AdditionTransformFunction (plus) in core/operator/transform/function/. Pinot evaluates these in
+ * double; with two INT operands the device sums the exact int64 value (equal to the reference's
+ * double sum while partial sums stay below 2^53), otherwise it computes in double as the
+ * reference does. Needs the query-specialised (hipRTC) kernel; EUNSUPPORTED without it. */
+enum pinot_amd_expr_op { PINOT_AMD_EXPR_COLUMN = 0, PINOT_AMD_EXPR_MUL = 1, PINOT_AMD_EXPR_SUB = 2,
+                         PINOT_AMD_EXPR_ADD = 3 };
+int pinot_amd_query_add_aggregation_expr(pinot_amd_query* q, int32_t agg_type, int32_t expr_op, const char* column_a,
+                                         const char* column_b, int32_t* out_index);
 /* QueryOptions numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000). */
 int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit);
 

@@ -46,7 +46,10 @@ class OLeaf(C.Structure):
 
 
 class OAgg(C.Structure):
-    _fields_ = [("func", C.c_int32), ("column", C.c_int32)]
+    _fields_ = [("func", C.c_int32), ("column", C.c_int32), ("expr", C.c_int32), ("column2", C.c_int32)]
+
+
+EXPR = {"COL": 0, "MUL": 1, "SUB": 2, "ADD": 3}
 
 
 _lib = None
@@ -308,15 +311,21 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
         slots = []
         for a in qc.aggregations:
             if a.func == "AVG":
-                nat.append(("SUM", a.column))
-                nat.append(("COUNT", "*"))
+                nat.append(("SUM", a.column, a.expr))
+                nat.append(("COUNT", "*", None))
                 slots.append(("avg", len(nat) - 2, len(nat) - 1))
             else:
-                nat.append((a.func, a.column))
+                nat.append((a.func, a.column, a.expr))
                 slots.append(("direct", len(nat) - 1))
         if not nat:
-            nat.append(("COUNT", "*"))
-        aggs = (OAgg * len(nat))(*[OAgg(AGG[f], -1 if c == "*" else os_.index[c]) for f, c in nat])
+            nat.append(("COUNT", "*", None))
+        def oagg(f, c, e):
+            if c == "*":
+                return OAgg(AGG[f], -1, 0, -1)
+            if e is None or e[0] == "COL":
+                return OAgg(AGG[f], os_.index[c if e is None else e[1]], 0, -1)
+            return OAgg(AGG[f], os_.index[e[1]], EXPR[e[0]], os_.index[e[2]])
+        aggs = (OAgg * len(nat))(*[oagg(f, c, e) for f, c, e in nat])
         bptr = _ptr(bits) if bits is not None else None
         if qc.group_by:
             cap = max(cnt, 1)

@@ -153,6 +153,20 @@ static double value_f64(const oracle_column* c, int64_t doc) {
   }
 }
 
+/* value of an aggregation's expression as the transform function yields it (double): the column
+ * value, or MULT = 1.0 * a * b (MultiplicationTransformFunction.java: literal product, then each
+ * argument in order), SUB = a - b (SubtractionTransformFunction.java), ADD = 0.0 + a + b
+ * (AdditionTransformFunction.java) */
+static double agg_f64(const oracle_column* cols, const oracle_agg* a, int64_t doc) {
+  const double x = value_f64(&cols[a->column], doc);
+  switch (a->expr) {
+    case OR_EXPR_MUL: return 1.0 * x * value_f64(&cols[a->column2], doc);
+    case OR_EXPR_SUB: return x - value_f64(&cols[a->column2], doc);
+    case OR_EXPR_ADD: return 0.0 + x + value_f64(&cols[a->column2], doc);
+    default: return x;
+  }
+}
+
 /* LZ4 block decoding as lz4-java's LZ4FastDecompressor does it (org.lz4:lz4-java 1.11.0, pom.xml:186,
  * third-party): the chunk decompressor behind ChunkCompressionType.LZ4
  * (pinot-segment-local/.../io/compression/LZ4Decompressor.java). Returns bytes written or -1. */
@@ -382,7 +396,7 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
           break;
         case OR_AGG_SUM: {
           double s = 0;
-          for (int32_t i = 0; i < len; i++) s += value_f64(c, block[i]);
+          for (int32_t i = 0; i < len; i++) s += agg_f64(cols, &aggs[a], block[i]);
           holder[a] = s + holder[a];
           break;
         }
@@ -394,18 +408,18 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
         }
         case OR_AGG_MIN: {
           double m = INFINITY;
-          for (int32_t i = 0; i < len; i++) m = fmin(m, value_f64(c, block[i]));
+          for (int32_t i = 0; i < len; i++) m = fmin(m, agg_f64(cols, &aggs[a], block[i]));
           /* Math.min propagates NaN; fmin does not */
           for (int32_t i = 0; i < len; i++)
-            if (isnan(value_f64(c, block[i]))) m = NAN;
+            if (isnan(agg_f64(cols, &aggs[a], block[i]))) m = NAN;
           holder[a] = (isnan(m) || isnan(holder[a])) ? NAN : fmin(m, holder[a]);
           break;
         }
         case OR_AGG_MAX: {
           double m = -INFINITY;
-          for (int32_t i = 0; i < len; i++) m = fmax(m, value_f64(c, block[i]));
+          for (int32_t i = 0; i < len; i++) m = fmax(m, agg_f64(cols, &aggs[a], block[i]));
           for (int32_t i = 0; i < len; i++)
-            if (isnan(value_f64(c, block[i]))) m = NAN;
+            if (isnan(agg_f64(cols, &aggs[a], block[i]))) m = NAN;
           holder[a] = (isnan(m) || isnan(holder[a])) ? NAN : fmax(m, holder[a]);
           break;
         }
@@ -480,10 +494,10 @@ int64_t oracle_group_by(const oracle_column* cols, int64_t num_docs, const uint6
         int64_t* li = &hi[key * naggs + a];
         switch (aggs[a].func) {
           case OR_AGG_COUNT: *li += 1; *h = (double)*li; break;
-          case OR_AGG_SUM: *h = *h + value_f64(c, d); break;
+          case OR_AGG_SUM: *h = *h + agg_f64(cols, &aggs[a], d); break;
           case OR_AGG_SUMLONG: *li = (int64_t)((uint64_t)*li + (uint64_t)value_i64(c, d)); *h = (double)*li; break;
-          case OR_AGG_MIN: { double v = value_f64(c, d); if (v < *h) *h = v; break; }
-          case OR_AGG_MAX: { double v = value_f64(c, d); if (v > *h) *h = v; break; }
+          case OR_AGG_MIN: { double v = agg_f64(cols, &aggs[a], d); if (v < *h) *h = v; break; }
+          case OR_AGG_MAX: { double v = agg_f64(cols, &aggs[a], d); if (v > *h) *h = v; break; }
         }
       }
     }
@@ -552,19 +566,19 @@ int64_t oracle_group_by(const oracle_column* cols, int64_t num_docs, const uint6
           *h = (double)*hi;
           break;
         case OR_AGG_SUM:
-          *h = *h + value_f64(c, doc);
+          *h = *h + agg_f64(cols, &aggs[a], doc);
           break;
         case OR_AGG_SUMLONG:
           *hi = (int64_t)((uint64_t)*hi + (uint64_t)value_i64(c, doc));
           *h = (double)*hi;
           break;
         case OR_AGG_MIN: {
-          double v = value_f64(c, doc);
+          double v = agg_f64(cols, &aggs[a], doc);
           if (v < *h) *h = v;
           break;
         }
         case OR_AGG_MAX: {
-          double v = value_f64(c, doc);
+          double v = agg_f64(cols, &aggs[a], doc);
           if (v > *h) *h = v;
           break;
         }

@@ -57,9 +57,15 @@ typedef struct {
   const uint64_t* doc_bitset; /* OR_PRED_DOC_BITSET */
 } oracle_leaf;
 
+/* aggregated expression: a column, or a binary arithmetic transform of two columns
+ * (MultiplicationTransformFunction / SubtractionTransformFunction / AdditionTransformFunction:
+ * DOUBLE results) */
+enum { OR_EXPR_COL = 0, OR_EXPR_MUL = 1, OR_EXPR_SUB = 2, OR_EXPR_ADD = 3 };
 typedef struct {
   int32_t func;
   int32_t column;        /* -1 for COUNT(*) */
+  int32_t expr;          /* OR_EXPR_* */
+  int32_t column2;       /* second operand of a binary expression */
 } oracle_agg;
 
 /* ---- forward index ---- */

@@ -77,6 +77,8 @@ SIGNATURES = {
     "pinot_amd_query_add_group_by": (C.c_int, [_P, C.c_char_p]),
     "pinot_amd_query_add_aggregation": (C.c_int, [_P, C.c_int32, C.c_char_p, C.POINTER(C.c_int32)]),
     "pinot_amd_query_set_num_groups_limit": (C.c_int, [_P, C.c_int64]),
+    "pinot_amd_query_add_aggregation_expr": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
+                                                       C.POINTER(C.c_int32)]),
     "pinot_amd_result_num_groups_limit_reached": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "pinot_amd_execute": (C.c_int, [_P, _PP, C.c_int32, _P, _PP]),
     "pinot_amd_execute_filter": (C.c_int, [_P, _PP, C.c_int32, _P, _PP]),

@@ -561,7 +561,9 @@ struct PredSpec {
 
 struct AggSpec {
   int32_t type;
-  std::string column;  // empty for COUNT(*)
+  std::string column;   // empty for COUNT(*); first operand of an expression
+  int32_t expr = 0;     // pinot_amd_expr_op (PINOT_AMD_EXPR_COLUMN: the column itself)
+  std::string column2;  // second operand of an expression
 };
 
 struct pinot_amd_query {
@@ -633,6 +635,21 @@ int pinot_amd_query_add_aggregation(pinot_amd_query* q, int32_t agg_type, const 
     return fail(PINOT_AMD_EINVAL, "add_aggregation: bad type");
   AggSpec a{agg_type, (column && strcmp(column, "*") != 0) ? column : ""};
   if (agg_type != PINOT_AMD_AGG_COUNT && a.column.empty()) return fail(PINOT_AMD_EINVAL, "add_aggregation: column required");
+  if (out_index) *out_index = (int32_t)q->aggs.size();
+  q->aggs.push_back(a);
+  return 0;
+}
+
+int pinot_amd_query_add_aggregation_expr(pinot_amd_query* q, int32_t agg_type, int32_t expr_op, const char* column_a,
+                                         const char* column_b, int32_t* out_index) {
+  if (!q || !column_a || !column_b || !*column_a || !*column_b)
+    return fail(PINOT_AMD_EINVAL, "add_aggregation_expr: bad arguments");
+  if (expr_op < PINOT_AMD_EXPR_MUL || expr_op > PINOT_AMD_EXPR_ADD)
+    return fail(PINOT_AMD_EINVAL, "add_aggregation_expr: bad expression op %d", expr_op);
+  if (agg_type != PINOT_AMD_AGG_SUM && agg_type != PINOT_AMD_AGG_MIN && agg_type != PINOT_AMD_AGG_MAX &&
+      agg_type != PINOT_AMD_AGG_AVG)
+    return fail(PINOT_AMD_EUNSUPPORTED, "add_aggregation_expr: aggregation %d over an expression", agg_type);
+  AggSpec a{agg_type, column_a, expr_op, column_b};
   if (out_index) *out_index = (int32_t)q->aggs.size();
   q->aggs.push_back(a);
   return 0;
@@ -1103,7 +1120,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     };
     for (auto& p : Q.preds) if (int rc = need(p.column)) return rc;
     for (auto& g : Q.group_by) if (int rc = need(g)) return rc;
-    for (auto& a : Q.aggs) if (!a.column.empty()) if (int rc = need(a.column)) return rc;
+    for (auto& a : Q.aggs) {
+      if (!a.column.empty()) if (int rc = need(a.column)) return rc;
+      if (!a.column2.empty()) if (int rc = need(a.column2)) return rc;
+    }
   }
   // group-by + aggregation columns always need decoding; predicate columns only if some segment's
   // leaf reads values (decided below)
@@ -1114,9 +1134,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   for (auto& a : Q.aggs) {
     if (a.column.empty()) continue;
-    const Column& c = *segs[0]->cols.at(a.column);
-    if (c.type == T_STRING) return fail(PINOT_AMD_EINVAL, "cannot aggregate STRING column %s", a.column.c_str());
-    slot_of(a.column);
+    for (const std::string* col : {&a.column, &a.column2}) {
+      if (col->empty()) continue;
+      const Column& c = *segs[0]->cols.at(*col);
+      if (c.type == T_STRING) return fail(PINOT_AMD_EINVAL, "cannot aggregate STRING column %s", col->c_str());
+      slot_of(*col);
+    }
   }
 
   // ---- per-segment leaves ----
@@ -1131,7 +1154,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const Column& c = *segs[si]->cols.at(p.column);
       bool needs_slot = false;
       bool decoded_anyway = std::find(Q.group_by.begin(), Q.group_by.end(), p.column) != Q.group_by.end();
-      for (auto& a : Q.aggs) decoded_anyway |= a.column == p.column;
+      for (auto& a : Q.aggs) decoded_anyway |= a.column == p.column || a.column2 == p.column;
       int rc = make_leaf_for_segment(r, si, segs[si], p, c, -1, &seg_leaves[si][pi], &needs_slot, r->stream,
                                      decoded_anyway);
       if (rc) return rc;
@@ -1195,18 +1218,25 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   q.num_keys = num_keys;
 
   // ---- accumulators: acc 0 = COUNT; others grouped by slot ----
-  struct AccReq { int slot; int op; };
+  struct AccReq { int slot; int op; int expr; int slot2; };
   std::vector<AccReq> reqs;
   std::vector<int> agg_req(Q.aggs.size(), -1);
+  bool any_expr = false;
   for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
     const AggSpec& a = Q.aggs[ai];
     if (a.type == PINOT_AMD_AGG_COUNT) continue;
     const Column& c = *segs[0]->cols.at(a.column);
+    // an expression sums exactly in int64 when both operands are INT (every partial sum of the
+    // reference's double accumulation is then exact below 2^53), otherwise in double
+    const bool expr_int = a.expr != PINOT_AMD_EXPR_COLUMN && c.type == T_INT &&
+                          segs[0]->cols.at(a.column2)->type == T_INT;
+    any_expr |= a.expr != PINOT_AMD_EXPR_COLUMN;
     int op;
     switch (a.type) {
       case PINOT_AMD_AGG_SUM:
       case PINOT_AMD_AGG_AVG:
-        op = is_float(c.type) ? ACC_SUM_F64 : ACC_SUM_I64;
+        if (a.expr != PINOT_AMD_EXPR_COLUMN) op = expr_int ? ACC_SUM_I64 : ACC_SUM_F64;
+        else op = is_float(c.type) ? ACC_SUM_F64 : ACC_SUM_I64;
         break;
       case PINOT_AMD_AGG_SUMLONG:
         if (is_float(c.type)) return fail(PINOT_AMD_EINVAL, "SUMLONG on floating column %s", a.column.c_str());
@@ -1216,17 +1246,19 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       default: op = ACC_MAX; break;
     }
     const int sl = slot_of(a.column);
+    const int sl2 = a.expr != PINOT_AMD_EXPR_COLUMN ? slot_of(a.column2) : -1;
     int found = -1;
     for (size_t k = 0; k < reqs.size(); ++k)
-      if (reqs[k].slot == sl && reqs[k].op == op) found = (int)k;
+      if (reqs[k].slot == sl && reqs[k].op == op && reqs[k].expr == a.expr && reqs[k].slot2 == sl2) found = (int)k;
     if (found < 0) {
-      reqs.push_back({sl, op});
+      reqs.push_back({sl, op, a.expr, sl2});
       found = (int)reqs.size() - 1;
     }
     agg_req[ai] = found;
   }
   if ((int)reqs.size() + 1 > kMaxAcc) return fail(PINOT_AMD_EUNSUPPORTED, "too many aggregations");
   std::vector<int> req_acc(reqs.size());
+  std::vector<AccReq> acc_req(kMaxAcc, AccReq{0, 0, 0, -1});  // accumulator index -> its request
   q.nacc = 1;
   q.acc_op[0] = ACC_COUNT;
   for (int sl = 0; sl < kMaxSlots; ++sl) {
@@ -1234,6 +1266,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (size_t k = 0; k < reqs.size(); ++k)
       if (reqs[k].slot == sl) {
         req_acc[k] = q.nacc;
+        acc_req[q.nacc] = reqs[k];
         q.acc_op[q.nacc++] = reqs[k].op;
       }
   }
@@ -1373,11 +1406,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.group.push_back({sl, r->key_stride[j]});
       for (int si = 0; si < n; ++si) jp.any_remap |= r->hsegs[si].cols[sl].remap != nullptr;
     }
-    for (int a = 1; a < q.nacc; ++a) {
-      int sl = 0;
-      while (sl < kMaxSlots && !(a >= q.slot_acc_begin[sl] && a < q.slot_acc_begin[sl + 1])) ++sl;
-      jp.accs.push_back({q.acc_op[a], sl});
-    }
+    for (int a = 1; a < q.nacc; ++a)
+      jp.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2});
     jp.num_keys = num_keys;
     jp.lds = q.lds_keys > 0;
     jp.bitset = filter_only;
@@ -1404,8 +1434,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         jp.key_shift = shift;
         jp.nparts = (int)nparts;
         for (auto& a : jp.accs)
-          if (std::find(jp.val_slots.begin(), jp.val_slots.end(), a.slot) == jp.val_slots.end())
-            jp.val_slots.push_back(a.slot);
+          if (std::find(jp.vals.begin(), jp.vals.end(), a.val()) == jp.vals.end()) jp.vals.push_back(a.val());
         jit_layout_records(&jp);
         // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a
         // run is too short to pay for the staging round trip and records are written directly
@@ -1420,6 +1449,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     } else {
       r->jit_status = "segments disagree on a column's encoding";
     }
+    if (!r->jit && any_expr)  // the generic AOT kernel reads plain columns only: fail loudly
+      return fail(PINOT_AMD_EUNSUPPORTED, "aggregation over an expression needs the query-specialised kernel (%s)",
+                  r->jit_status.c_str());
     if (r->jit && jp.partitioned) {
       r->partitioned = true;
       r->part.nparts = jp.nparts;

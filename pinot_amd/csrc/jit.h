@@ -24,9 +24,21 @@ struct JitLeaf {
   int negate;
   uint32_t kinds;  // bit k set: some segment resolves this predicate to LEAF kind k
 };
+// value an accumulator reads: a column slot, or a binary arithmetic expression of two slots
+// (EXPR_MUL / SUB / ADD: Pinot's times / minus / plus transforms)
+enum { EXPR_COL = 0, EXPR_MUL = 1, EXPR_SUB = 2, EXPR_ADD = 3 };
+struct JitVal {
+  int expr = EXPR_COL;
+  int slot = 0;
+  int slot2 = -1;
+  bool operator==(const JitVal& o) const { return expr == o.expr && slot == o.slot && slot2 == o.slot2; }
+};
 struct JitAcc {
   int op;    // ACC_*
   int slot;
+  int expr = EXPR_COL;
+  int slot2 = -1;
+  JitVal val() const { return JitVal{expr, slot, slot2}; }
 };
 struct JitPlan {
   std::vector<JitSlot> slots;
@@ -43,12 +55,12 @@ struct JitPlan {
   bool partitioned = false;
   int key_shift = 0;           // keys per partition = 2^key_shift
   int nparts = 0;
-  std::vector<int> val_slots;  // record value columns (slots read by accumulators)
+  std::vector<JitVal> vals;    // record values (distinct values read by accumulators)
   std::vector<int> val_off;    // byte offset of each value column in a record (key u32 at 0)
   int rec_bytes = 0;           // record size, multiple of 8
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
 };
-// record layout of a partitioned plan (fills val_off / rec_bytes from val_slots)
+// record layout of a partitioned plan (fills val_off / rec_bytes from vals)
 void jit_layout_records(JitPlan* p);
 // LDS bytes of the scatter pass for a staging capacity
 size_t jit_scatter_lds(const JitPlan& p, int cap);
@@ -59,9 +71,10 @@ struct JitKernel {
   hipFunction_t fn_scatter = nullptr;  // partitioned: scatter pass
   hipFunction_t fn_agg = nullptr;      // partitioned: LDS aggregation of the partitions
 };
-// record value column j of a partitioned plan: C type of the stored value
-const char* jit_val_ctype(const JitSlot& s);
-int jit_val_size(const JitSlot& s);
+// C type / size of an accumulated value: a column's decoded value type; an expression is int64
+// when both operands are INT (exact), else double (the transforms' DOUBLE result)
+const char* jit_val_ctype(const JitPlan& p, const JitVal& v);
+int jit_val_size(const JitPlan& p, const JitVal& v);
 
 std::string jit_shape_key(const JitPlan& p);
 std::string jit_generate(const JitPlan& p);

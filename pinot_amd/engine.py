@@ -31,6 +31,7 @@ TYPE_CODE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3, STRING: 4}
 ENC_CODE = {"FIXED_BIT": 0, "RAW": 1, "SORTED": 2}
 PRED_CODE = {"EQ": 0, "NOT_EQ": 1, "IN": 2, "NOT_IN": 3, "RANGE": 4}
 AGG_CODE = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4, "AVG": 5}
+EXPR_CODE = {"MUL": 1, "SUB": 2, "ADD": 3}
 
 
 def _stream_handle(stream) -> Optional[int]:
@@ -329,21 +330,26 @@ class ServerQueryExecutor:
             native = []
             agg_slots = []
 
-            def add(func, column):
+            def add(func, column, expr=None):
                 key = (func, column)
                 if key in native:
                     return native.index(key)
                 idx = C.c_int32()
-                check(L.pinot_amd_query_add_aggregation(qh, AGG_CODE[func], column.encode(), C.byref(idx)),
-                      f"add_aggregation({func})")
+                if expr is None:
+                    check(L.pinot_amd_query_add_aggregation(qh, AGG_CODE[func], column.encode(), C.byref(idx)),
+                          f"add_aggregation({func})")
+                else:
+                    check(L.pinot_amd_query_add_aggregation_expr(qh, AGG_CODE[func], EXPR_CODE[expr[0]],
+                                                                 expr[1].encode(), expr[2].encode(), C.byref(idx)),
+                          f"add_aggregation_expr({func} {column})")
                 native.append(key)
                 return idx.value
 
             for a in qc.aggregations:
                 if a.func == "AVG":
-                    agg_slots.append(("avg", add("SUM", a.column), add("COUNT", "*")))
+                    agg_slots.append(("avg", add("SUM", a.column, a.expr), add("COUNT", "*")))
                 else:
-                    agg_slots.append(("direct", add(a.func, a.column)))
+                    agg_slots.append(("direct", add(a.func, a.column, a.expr)))
             if not qc.aggregations and qc.group_by:
                 add("COUNT", "*")  # DISTINCT-style group-by still needs the group presence count
             arr = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])

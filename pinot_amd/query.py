@@ -95,15 +95,33 @@ def to_cnf(f: Optional[FilterContext]) -> List[List[Leaf]]:
     return cnf(nnf(f, False))
 
 
+EXPR_OPS = {"*": "MUL", "-": "SUB", "+": "ADD"}
+EXPR_FUNC = {"MUL": "times", "SUB": "minus", "ADD": "plus"}
+
+
 @dataclasses.dataclass
 class Aggregation:
+    """AggregationFunction over a column or a binary arithmetic transform of two columns.
+
+    column: "*" for COUNT(*), the column name, or the expression's canonical text
+    (``times(a,b)``, Pinot's FunctionContext names) for an expression argument.
+    expr: None for a plain column, else (op, column_a, column_b) with op MUL / SUB / ADD
+    (MultiplicationTransformFunction / SubtractionTransformFunction / AdditionTransformFunction;
+    CAST(x AS DOUBLE) operands are accepted: every transform already computes in double)."""
     func: str          # COUNT SUM MIN MAX AVG SUMLONG
-    column: str        # "*" for COUNT(*)
+    column: str
     alias: Optional[str] = None
+    expr: Optional[Tuple[str, str, str]] = None
 
     @property
     def name(self) -> str:
         return self.alias or f"{self.func.lower()}({self.column})"
+
+    @property
+    def columns(self) -> Tuple[str, ...]:
+        if self.column == "*":
+            return ()
+        return (self.expr[1], self.expr[2]) if self.expr else (self.column,)
 
 
 @dataclasses.dataclass
@@ -124,7 +142,7 @@ class QueryContext:
 
 # ---------------------------------------------------------------------------------------- parser
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+\.\d*(?:[eE][-+]?\d+)?|-?\d+(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')"
-                    r"|(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
+                    r"|(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*|\+|-)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
 
 
 def _tokenize(sql: str):
@@ -198,17 +216,26 @@ class _Parser:
             if tok[0] == "id" and tok[1].upper() in AGG_FUNCS and self.peek(1) == ("op", "("):
                 func = tok[1].upper()
                 self.i += 2
+                expr = None
                 if self.peek() == ("op", "*"):
                     self.i += 1
                     col = "*"
                 else:
-                    col = self.ident()
+                    col = self.operand()
+                    if self.peek()[0] == "op" and self.peek()[1] in EXPR_OPS:
+                        op = EXPR_OPS[self.peek()[1]]
+                        self.i += 1
+                        col2 = self.operand()
+                        expr = (op, col, col2)
+                        col = f"{EXPR_FUNC[op]}({col},{col2})"
                 self.eat_op(")")
                 alias = None
                 if self.kw("AS"):
                     self.i += 1
                     alias = self.ident()
-                aggs.append(Aggregation(func, col, alias))
+                elif self.peek()[0] == "id" and self.peek()[1].upper() not in ("FROM",):
+                    alias = self.ident()   # implicit alias: sum(x) revenue
+                aggs.append(Aggregation(func, col, alias, expr))
             else:
                 cols.append(self.ident())
             if self.peek() == ("op", ","):
@@ -243,6 +270,20 @@ class _Parser:
         if self.peek()[0] != "eof":
             raise ValueError(f"unexpected trailing token {self.peek()}")
         return QueryContext(table, aggs, group_by, flt, order, limit, cols)
+
+    def operand(self) -> str:
+        """A column, optionally as CAST(column AS type) (the cast does not change the value the
+        arithmetic transforms compute: they read every argument as double)."""
+        if self.kw("CAST") and self.peek(1) == ("op", "("):
+            self.i += 2
+            col = self.ident()
+            self.eat_kw("AS")
+            t = self.ident().upper()
+            if t not in ("DOUBLE", "FLOAT", "LONG", "INT", "BIGINT", "INTEGER"):
+                raise ValueError(f"unsupported CAST type {t}")
+            self.eat_op(")")
+            return col
+        return self.ident()
 
     def order_item(self):
         tok = self.peek()

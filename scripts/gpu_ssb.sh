@@ -1,0 +1,12 @@
+set -o pipefail
+mkdir -p gpurun_out
+true
+tail -2 gpurun_out/ssb_test.log
+timeout -k 10 700 python bench.py --workload ssb --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/ssb_bench.json 2> gpurun_out/ssb_bench.err || { echo BENCH_FAILED; tail -20 gpurun_out/ssb_bench.err; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/ssb_bench.json"):
+    d = json.loads(l)
+    print("%-60.60s sel %.5f value %.3e rows/s ms %.3f frac %.3f B/row %.2f %s" % (d["config"]["query"], d["config"]["selectivity"], d["value"], d["roofline"]["kernel_ms"], d["roofline"]["frac"], d["roofline"]["bytes_per_row"], d["config"]["scan_kernel"]))
+PY
+grep staged gpurun_out/ssb_bench.err | tail -1

@@ -92,6 +92,50 @@ def _decode(f, schema):
     raise NotImplementedError(schema)
 
 
+def snappy_decompress(src: bytes) -> bytes:
+    """Raw Snappy block decompression (the format's published spec: a varint uncompressed length,
+    then literal / copy-1 / copy-2 / copy-4 elements), for avro's "snappy" codec."""
+    pos, n, shift = 0, 0, 0
+    while True:
+        b = src[pos]
+        pos += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            break
+    out = bytearray()
+    while pos < len(src):
+        tag = src[pos]
+        pos += 1
+        kind = tag & 3
+        if kind == 0:  # literal
+            ln = tag >> 2
+            if ln >= 60:
+                nb = ln - 59
+                ln = int.from_bytes(src[pos:pos + nb], "little")
+                pos += nb
+            ln += 1
+            out += src[pos:pos + ln]
+            pos += ln
+            continue
+        if kind == 1:
+            ln = ((tag >> 2) & 7) + 4
+            off = ((tag >> 5) << 8) | src[pos]
+            pos += 1
+        elif kind == 2:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(src[pos:pos + 2], "little")
+            pos += 2
+        else:
+            ln = (tag >> 2) + 1
+            off = int.from_bytes(src[pos:pos + 4], "little")
+            pos += 4
+        for _ in range(ln):  # byte-serial: copies may overlap their own output
+            out.append(out[-off])
+    assert len(out) == n, (len(out), n)
+    return bytes(out)
+
+
 def read_avro(path):
     with open(path, "rb") as fh:
         f = io.BytesIO(fh.read())
@@ -108,7 +152,7 @@ def read_avro(path):
             k = _read_bytes(f).decode()
             meta[k] = _read_bytes(f)
     codec = meta.get("avro.codec", b"null").decode()
-    assert codec == "null", codec
+    assert codec in ("null", "snappy"), codec
     schema = json.loads(meta["avro.schema"])
     sync = f.read(16)
     rows = []
@@ -117,9 +161,13 @@ def read_avro(path):
             count = _read_long(f)
         except EOFError:
             break
-        _read_long(f)  # block byte size
+        size = _read_long(f)  # block byte size
+        block = f.read(size)
+        if codec == "snappy":  # snappy block followed by a 4-byte CRC32 of the uncompressed data
+            block = snappy_decompress(block[:-4])
+        bf = io.BytesIO(block)
         for _ in range(count):
-            rows.append(_decode(f, schema))
+            rows.append(_decode(bf, schema))
         assert f.read(16) == sync
     return schema, rows
 

@@ -54,3 +54,28 @@ def random_segment(rng, n, name="seg", bits_cards=(1000, 37), raw_types=(INT, LO
     if float_col:
         cols["fd"] = ((rng.integers(0, 20, n) * 0.25).astype(np.float64), DOUBLE, {})
     return build_segment(name, cols)
+
+
+def load_ssb_expected():
+    with open(os.path.join(GOLDEN, "ssb_expected.json")) as f:
+        return json.load(f)
+
+
+def ssb_flat_segment(name="lineorder_flat_0", split=None):
+    """The reference's SSB quickstart lineorder joined with its dimensions (tests/golden/ssb_flat.npz),
+    as Pinot would build it: every column dictionary-encoded except the raw INT metrics
+    (pinot_amd.ssb.FLAT_COLUMNS). split=k: k segments of consecutive rows instead of one."""
+    from pinot_amd.ssb import FLAT_COLUMNS
+    data = np.load(os.path.join(GOLDEN, "ssb_flat.npz"), allow_pickle=False)
+    n = len(data["LO_ORDERDATE"])
+    bounds = [0, n] if not split else [n * i // split for i in range(split + 1)]
+    segs = []
+    for i in range(len(bounds) - 1):
+        cols = {}
+        for c, t, dict_enc in FLAT_COLUMNS:
+            v = data[c][bounds[i]:bounds[i + 1]]
+            if t == STRING:
+                v = v.astype(object)
+            cols[c] = (v, t, {"dictionary": dict_enc, "detect_sorted": False})
+        segs.append(build_segment(f"{name}_{i}", cols))
+    return segs
