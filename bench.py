@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one segment against the oracle")
+    ap.add_argument("--query-index", type=int, default=None, help="run only this query of the workload")
     args = ap.parse_args()
 
     import torch
@@ -110,6 +111,8 @@ def main():
     from pinot_amd import dist as pdist, engine
     from pinot_amd.query import parse_sql
     gen, queries, bytes_per_row, workload_desc, distinct = workloads()[args.workload]
+    if args.query_index is not None:
+        queries = [queries[args.query_index]]
     if args.segments is None:
         args.segments = 60 if args.workload == "ssb" else 100
 

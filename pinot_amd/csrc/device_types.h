@@ -74,6 +74,7 @@ struct DevSegment {
 //   agg pass:     one LDS table of 2^key_shift keys per partition, flushed with global atomics
 struct DevPartition {
   int32_t nparts, key_shift;
+  int64_t atomic_threshold;  // records <= this: the direct-atomic scan runs instead of scatter + agg
   uint32_t* hist;
   int64_t* offs;
   int64_t* part_begin;

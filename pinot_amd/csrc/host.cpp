@@ -713,10 +713,13 @@ struct pinot_amd_result {
   // partitioned GROUP BY (JIT only): count -> offsets -> scatter -> per-partition LDS aggregation
   int64_t num_groups_limit = 100000;
   bool partitioned = false;
+  JitKernel* jit_atomic = nullptr;  // partitioned plans: direct-atomic scan used when few docs match
+  int atomic_grid = 1;
   DevPartition part{};
   DevBuf hist, offs, part_begin, rec;
   int rec_bytes = 0, stage_cap = 0;
   int agg_grid = 1;
+  int scan_nsub = 1;            // JIT scan: 256-thread groups per block (4: CU-wide block, large LDS table)
   size_t shmem_scatter = 0, shmem_agg = 0;
   ~pinot_amd_result() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -1070,6 +1073,8 @@ static int run_plan(pinot_amd_result* r) {
     const unsigned count_grid = (unsigned)(r->grid * kPartCountRatio);
     HIP_OK(hipModuleLaunchKernel(r->jit->fn, count_grid, 1, 1, pt, 1, 1, (unsigned)r->shmem, st, args, nullptr));
     HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, count_grid, r->part.offs, r->part.part_begin, st));
+    if (r->jit_atomic)
+      HIP_OK(hipModuleLaunchKernel(r->jit_atomic->fn, (unsigned)r->atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
     HIP_OK(hipModuleLaunchKernel(r->jit->fn_scatter, (unsigned)r->grid, 1, 1, pt, 1, 1, (unsigned)r->shmem_scatter, st,
                                  args, nullptr));
     void* agg_args[] = {(void*)&r->part, (void*)&acc};
@@ -1081,7 +1086,7 @@ static int run_plan(pinot_amd_result* r) {
     uint64_t* const* bits = r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p;
     unsigned long long* matched = (unsigned long long*)r->matched.p;
     void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock, 1, 1, (unsigned)r->shmem, st, args,
+    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock * r->scan_nsub, 1, 1, (unsigned)r->shmem, st, args,
                                  nullptr));
   } else {
     HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p,
@@ -1374,6 +1379,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   if (rc) return rc;
 
   // query-specialised kernel (hipRTC): needs every slot's encoding to agree across the batch
+  bool jp_lds = false;
+  int jp_scan_nsub = 1;
   {
     JitPlan jp;
     bool ok = true;
@@ -1409,13 +1416,18 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (int a = 1; a < q.nacc; ++a)
       jp.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2});
     jp.num_keys = num_keys;
+    // pipeline depth from the bytes a wave has in flight per tile (256 docs x bytes per row):
+    // aim for ~4 KiB per wave (~64-96 KiB per CU at 16-24 resident waves) to cover HBM latency
+    {
+      double bpr = 0;
+      for (const JitSlot& js : jp.slots)
+        bpr += js.enc == ENC_FIXED_BIT ? (js.bits > 0 ? js.bits : 16) / 8.0 : js.enc == ENC_RAW ? value_size(js.type) : 0.0;
+      jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
+      if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(4, atoi(pd)));
+    }
     jp.lds = q.lds_keys > 0;
     jp.bitset = filter_only;
     jp.aggregate = q.nacc > 0;
-    // key space too large for an LDS table: partition the matching docs by key range and
-    // aggregate each partition in LDS (per-lane HBM atomics on random keys run ~17x below the
-    // coalesced atomic rate). Keys per partition: the largest power of two whose nacc tables fit
-    // in one workgroup's LDS (gfx950: 160 KiB); local keys are 16-bit.
     int lds_max = 0;
     {
       int dev = 0;
@@ -1423,6 +1435,19 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) lds_max = 65536;
       lds_max = std::min(lds_max, 160 * 1024);
     }
+    // group table above the 40 KiB that keeps four 256-thread blocks per CU but within one
+    // workgroup's LDS: one CU-wide block (4 x 256 threads, 16 waves) owns the whole table
+    if (!jp.lds && q.nacc > 0 && !filter_only && lds_bytes <= lds_max) {
+      const char* wl = getenv("PINOT_AMD_WIDE_LDS");
+      if (!(wl && strcmp(wl, "0") == 0)) {
+        jp.lds = true;
+        jp.scan_nsub = kPartSub;
+      }
+    }
+    // key space too large for an LDS table: partition the matching docs by key range and
+    // aggregate each partition in LDS (per-lane HBM atomics on random keys run ~17x below the
+    // coalesced atomic rate). Keys per partition: the largest power of two whose nacc tables fit
+    // in one workgroup's LDS (gfx950: 160 KiB); local keys are 16-bit.
     const char* pe = getenv("PINOT_AMD_PARTITIONED");
     const bool allow_part = !(pe && strcmp(pe, "0") == 0);
     if (ok && allow_part && !filter_only && q.nacc > 0 && !jp.lds && !Q.group_by.empty()) {
@@ -1449,10 +1474,31 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     } else {
       r->jit_status = "segments disagree on a column's encoding";
     }
+    jp_lds = jp.lds && !jp.partitioned;
+    jp_scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
     if (!r->jit && any_expr)  // the generic AOT kernel reads plain columns only: fail loudly
       return fail(PINOT_AMD_EUNSUPPORTED, "aggregation over an expression needs the query-specialised kernel (%s)",
                   r->jit_status.c_str());
     if (r->jit && jp.partitioned) {
+      // companion direct-atomic scan for batches where the filter keeps few docs (decided on the
+      // device from the count pass): atomics on so few keys cost less than writing records
+      JitPlan ja = jp;
+      ja.partitioned = false;
+      ja.lds = false;
+      ja.scan_nsub = 1;
+      ja.atomic_gate = true;
+      ja.vals.clear();
+      ja.val_off.clear();
+      ja.rec_bytes = ja.stage_cap = ja.nparts = ja.key_shift = 0;
+      const char* ag = getenv("PINOT_AMD_ATOMIC_HANDOVER");
+      if (!(ag && strcmp(ag, "0") == 0)) {
+        std::string err;
+        r->jit_atomic = jit_get(ja, &err);
+      }
+      int64_t docs = 0;
+      for (auto* s : segs) docs += s->num_docs;
+      r->part.atomic_threshold = r->jit_atomic ? docs / 64 : -1;
+      if (ag && strcmp(ag, "force") == 0 && r->jit_atomic) r->part.atomic_threshold = INT64_MAX;
       r->partitioned = true;
       r->part.nparts = jp.nparts;
       r->part.key_shift = jp.key_shift;
@@ -1467,7 +1513,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       r->stage_cap = jp.stage_cap;
     }
   }
-  r->shmem = q.lds_keys > 0 ? (size_t)lds_bytes : 0;
+  r->scan_nsub = r->jit ? jp_scan_nsub : 1;
+  r->shmem = (q.lds_keys > 0 || (r->jit && jp_lds)) ? (size_t)lds_bytes : 0;
   if (r->partitioned) r->shmem = (size_t)r->part.nparts * 4;
 
   // persistent grid: enough blocks to fill every CU at the occupancy the LDS table allows
@@ -1488,9 +1535,16 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         na < 1)
       na = 1;
     r->agg_grid = cus * na;
+    if (r->jit_atomic) {
+      int nt = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nt, r->jit_atomic->fn, kBlock, 0) != hipSuccess || nt < 1)
+        nt = 1;
+      r->atomic_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nt, tiles));
+    }
   } else if (r->jit) {
     int nb = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock, r->shmem) != hipSuccess || nb < 1)
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock * r->scan_nsub, r->shmem) !=
+            hipSuccess || nb < 1)
       nb = 1;
     per_cu = nb;
   } else {
@@ -1498,7 +1552,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   int64_t grid = (int64_t)cus * per_cu;
   if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
-  if (r->partitioned && grid * kPartSub > tiles) grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
+  if ((r->partitioned || r->scan_nsub > 1) && grid * kPartSub > tiles)
+    grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
   r->grid = (int)grid;
   if (r->partitioned) {
     const size_t cells = (size_t)r->part.nparts * (size_t)grid * kPartCountRatio;

@@ -49,8 +49,13 @@ struct JitPlan {
   std::vector<JitAcc> accs;  // accumulators 1..n (0 is COUNT), in DevQuery acc order
   int64_t num_keys = 1;
   bool lds = false;
+  int scan_nsub = 1;           // 256-thread groups per scan block (4 for a table above 40 KiB)
+  int depth = 1;               // software-pipeline depth (tiles prefetched ahead), 1..4
   bool bitset = false;
   bool aggregate = true;
+  // direct-atomic scan paired with a partitioned plan: runs only when the count pass found at most
+  // part.atomic_threshold matching docs (then scatter + agg exit at once); counts no docs itself
+  bool atomic_gate = false;
   // partitioned GROUP BY (DevPartition): count / scatter / LDS-aggregate kernels instead of one scan
   bool partitioned = false;
   int key_shift = 0;           // keys per partition = 2^key_shift

@@ -57,15 +57,17 @@ def test_highcard_partitioned_vs_oracle(engine, qi, n, monkeypatch):
     assert_same_groups(res.groups(), og, _fsum(qc))
 
 
-@pytest.mark.parametrize("stage_cap", [None, "0", "4"])
-def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch, stage_cap):
+@pytest.mark.parametrize("stage_cap,handover", [(None, "0"), ("0", "0"), ("4", "0"), (None, "force"), (None, None)])
+def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch, stage_cap, handover):
     """Same query through the partitioned plan and the direct HBM-atomic plan: identical groups.
     stage_cap: scatter records staged per partition in LDS (None: planner's choice; 0: direct
-    writes; 4: tiny staging, most records take the overflow path)."""
-    if stage_cap is None:
-        monkeypatch.delenv("PINOT_AMD_STAGE_CAP", raising=False)
-    else:
-        monkeypatch.setenv("PINOT_AMD_STAGE_CAP", stage_cap)
+    writes; 4: tiny staging, most records take the overflow path). handover: the partitioned
+    plan's device-side switch to its direct-atomic scan ("force": always, "0": never)."""
+    for var, val in (("PINOT_AMD_STAGE_CAP", stage_cap), ("PINOT_AMD_ATOMIC_HANDOVER", handover)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, val)
     rng = np.random.default_rng(77)
     bufs = [random_segment(rng, 200_000 + 999 * i, name=f"s{i}", bits_cards=(1000, 700)) for i in range(3)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
@@ -124,3 +126,21 @@ def test_num_groups_limit_reached_flag(engine, monkeypatch):
     res = engine.ServerQueryExecutor().execute(
         "SELECT d0, d1, COUNT(*) FROM t GROUP BY d0, d1 OPTION(numGroupsLimit=1000)", [seg])
     assert res.num_groups_limit_reached() is True
+
+
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_wide_lds_table_plan(engine, monkeypatch, wide):
+    """A group table between 40 KiB and the 160 KiB workgroup LDS runs in one CU-wide block per CU
+    (PINOT_AMD_WIDE_LDS=0: the partitioned plan instead); both equal the oracle."""
+    monkeypatch.setenv("PINOT_AMD_JIT", "1")
+    monkeypatch.setenv("PINOT_AMD_WIDE_LDS", wide)
+    rng = np.random.default_rng(21)
+    bufs = [random_segment(rng, 250_000 + 17 * i, name=f"w{i}", bits_cards=(1000, 5)) for i in range(2)]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = ("SELECT d0, d1, COUNT(*), SUM(r_long), MAX(r_double), MIN(r_int) FROM t WHERE r_int > -500000 "
+         "GROUP BY d0, d1 OPTION(numGroupsLimit=1000000)")
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert res.kernel_info() == ("jit" if wide == "1" else "jit-partitioned"), res.kernel_info()
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)

@@ -373,3 +373,24 @@ def test_fixed_bit_widths_through_scan(engine, bits, generic, monkeypatch):
     nm, og = oracle.execute(q, bufs)
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("depth", ["1", "2", "3", "4"])
+def test_pipeline_depths_across_segment_boundaries(engine, depth, monkeypatch):
+    """The JIT scan's software pipeline (tiles prefetched ahead, crossing segment boundaries and
+    ragged segment tails) gives identical results at every depth."""
+    monkeypatch.setenv("PINOT_AMD_JIT", "1")
+    monkeypatch.setenv("PINOT_AMD_PREFETCH", depth)
+    rng = np.random.default_rng(int(depth))
+    bufs = [random_segment(rng, n, name=f"pd{i}", bits_cards=(300, 9)) for i, n in
+            enumerate((1, 1023, 1025, 4097, 100_003, 7))]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    for q in ["SELECT d1, COUNT(*), SUM(r_long), MAX(r_double), MIN(r_int) FROM t WHERE d0 < 200 GROUP BY d1",
+              "SELECT COUNT(*), SUM(r_int), SUM(r_double) FROM t WHERE r_long > 0 OR d1 IN (3, 17)"]:
+        res = engine.ServerQueryExecutor().execute(q, segs)
+        nm, og = oracle.execute(q, bufs)
+        assert res.num_docs_matched() == nm
+        from pinot_amd.query import parse_sql
+        qc = parse_sql(q)
+        fsum = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "r_double"}
+        assert_same_groups(res.groups(), og, fsum)
