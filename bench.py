@@ -55,25 +55,29 @@ def workloads():
     }
 
 
-def cpu_baseline(workload: str, query: str, seg_rows: int, seconds: float):
-    """Time the CPU oracle (scalar C port of the reference path, 1 core) on freshly generated
-    segments of the same workload until `seconds` of CPU work have run."""
+def cpu_baseline(workload: str, query: str, seg_rows: int, seconds: float, threads: int):
+    """Time the CPU oracle (scalar C restatement of the reference path) on the host cores: `threads`
+    segments of the same workload are generated once, then run concurrently, one per thread
+    (the C calls release the GIL), round after round until `seconds` of wall time have passed —
+    the shape of Pinot's server executing one segment per worker thread."""
+    import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     gen = workloads()[workload][0]
+    bufs = [gen(f"cpu{k}", seg_rows, seed=10_000 + k) for k in range(threads)]
     rows = 0
-    t_cpu = 0.0
-    k = 0
-    while t_cpu < seconds and k < 64:
-        bufs = gen(f"cpu{k}", seg_rows, seed=10_000 + k)
+    rounds = 0
+    with cf.ThreadPoolExecutor(max_workers=threads) as pool:
         t0 = time.perf_counter()
-        oracle.execute(query, [bufs])
-        t_cpu += time.perf_counter() - t0
-        rows += seg_rows
-        k += 1
-    return {"value": rows / t_cpu, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{k} segments x {seg_rows} rows of the same table and query, oracle/pinot_oracle.c "
-                      f"(scalar restatement of the reference Java path), {t_cpu:.1f} s"}
+        while rounds == 0 or time.perf_counter() - t0 < seconds:
+            list(pool.map(lambda b: oracle.execute(query, [b]), bufs))
+            rows += threads * seg_rows
+            rounds += 1
+        wall = time.perf_counter() - t0
+    return {"value": rows / wall, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} rounds x {threads} segments x {seg_rows} rows of the same table and query, one "
+                      f"segment per thread, oracle/pinot_oracle.c (scalar C restatement of the reference Java "
+                      f"path), {wall:.1f} s wall"}
 
 
 def query_bytes_per_row(query: str, seg) -> float:
@@ -101,6 +105,8 @@ def main():
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default 100; ssb: 60 = SF100)")
     ap.add_argument("--rows", type=int, default=10_000_000, help="rows per segment")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the CPU baseline (the GPU box's CPU share per GPU is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify one segment against the oracle")
     ap.add_argument("--query-index", type=int, default=None, help="run only this query of the workload")
@@ -230,7 +236,8 @@ def main():
             cpu = None
             if not args.no_cpu_baseline and world == 1:
                 log("[rank 0] timing the CPU baseline ...")
-                cpu = cpu_baseline(args.workload, query, min(args.rows, 10_000_000), args.cpu_seconds)
+                cpu = cpu_baseline(args.workload, query, min(args.rows, 10_000_000), args.cpu_seconds,
+                                   max(1, min(args.cpu_threads, os.cpu_count() or 1)))
             out = {
                 "metric": METRIC,
                 "value": value,
