@@ -1387,7 +1387,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (int sl = 0; sl < nslots && ok; ++sl) {
       const int enc = r->hsegs[0].cols[sl].enc;
       for (int si = 1; si < n; ++si) ok &= r->hsegs[si].cols[sl].enc == enc;
-      JitSlot js{enc, r->hsegs[0].cols[sl].type, 0};
+      JitSlot js{enc, r->hsegs[0].cols[sl].type, 0, 0};
+      if (enc != ENC_RAW) {  // dictionary of <= 64 entries everywhere: lane-register table
+        bool small = true;
+        for (int si = 0; si < n; ++si) small &= r->hsegs[si].cols[sl].card <= 64 && r->hsegs[si].cols[sl].card > 0;
+        js.dict_regs = small ? 1 : 0;
+      }
       if (enc == ENC_FIXED_BIT) {
         // bit width shared by the whole batch (and <= 15): decode with compile-time shifts
         js.bits = r->hsegs[0].cols[sl].bits;
@@ -1401,10 +1406,14 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     for (size_t k = 0; k < order.size(); ++k) {
       JitLeaf jl{pred_slot[order[k]], Q.preds[order[k]].clause, r->hsegs[0].leaves[k].negate, 0u};
+      bool small_sets = jl.slot >= 0;
       for (int si = 0; si < n; ++si) {
         ok &= r->hsegs[si].leaves[k].negate == jl.negate;
         jl.kinds |= 1u << r->hsegs[si].leaves[k].kind;
+        if (jl.slot >= 0) small_sets &= r->hsegs[si].cols[jl.slot].card < 64 * 32;
       }
+      // dictId-set bitmask of <= 64 words in every segment: one word per lane
+      jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
       jp.leaves.push_back(jl);
     }
     jp.nclauses = nclauses;
@@ -1424,6 +1433,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         bpr += js.enc == ENC_FIXED_BIT ? (js.bits > 0 ? js.bits : 16) / 8.0 : js.enc == ENC_RAW ? value_size(js.type) : 0.0;
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
       if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(4, atoi(pd)));
+      if (const char* lr = getenv("PINOT_AMD_LANE_TABLES"))
+        if (strcmp(lr, "0") == 0) {
+          for (auto& js : jp.slots) js.dict_regs = 0;
+          for (auto& jl : jp.leaves) jl.bits_regs = 0;
+        }
+      if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
     }
     jp.lds = q.lds_keys > 0;
     jp.bitset = filter_only;

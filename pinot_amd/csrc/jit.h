@@ -17,12 +17,14 @@ struct JitSlot {
   int enc;       // ENC_* (the same in every segment of the batch)
   int type;      // T_* value type
   int bits = 0;  // FIXED_BIT: bit width when every segment of the batch agrees (<= 15), else 0
+  int dict_regs = 0;  // dictionary of <= 64 entries in every segment: looked up across lanes (ds_bpermute)
 };
 struct JitLeaf {
   int slot;        // -1: reads no column (docId range / bitset / constant)
   int clause;
   int negate;
   uint32_t kinds;  // bit k set: some segment resolves this predicate to LEAF kind k
+  int bits_regs = 0;  // dictId set of <= 64 words in every segment: held one word per lane
 };
 // value an accumulator reads: a column slot, or a binary arithmetic expression of two slots
 // (EXPR_MUL / SUB / ADD: Pinot's times / minus / plus transforms)
@@ -51,6 +53,7 @@ struct JitPlan {
   bool lds = false;
   int scan_nsub = 1;           // 256-thread groups per scan block (4 for a table above 40 KiB)
   int depth = 1;               // software-pipeline depth (tiles prefetched ahead), 1..4
+  int waves_per_eu = 0;        // > 0: occupancy target handed to the register allocator
   bool bitset = false;
   bool aggregate = true;
   // direct-atomic scan paired with a partitioned plan: runs only when the count pass found at most

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+for qi in 0 10 6; do for d in 1 2 3 4; do
+PINOT_AMD_PREFETCH=$d timeout -k 10 300 python bench.py --workload ssb --query-index $qi --segments 20 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/sd.json 2> gpurun_out/sd.err || exit 1
+python -c "import json; d=json.load(open('gpurun_out/sd.json')); print('q $qi depth $d', round(d['roofline']['kernel_ms'],4))"
+done; done
