@@ -75,6 +75,8 @@ struct DevSegment {
 struct DevPartition {
   int32_t nparts, key_shift;
   int64_t atomic_threshold;  // records <= this: the direct-atomic scan runs instead of scatter + agg
+  int64_t sample_stride;     // > 0: counts[1] x stride estimates the matches before the count pass
+  unsigned long long* counts;  // [0] count-pass matches, [1] sampled matches, [2] direct-atomic scan matches
   uint32_t* hist;
   int64_t* offs;
   int64_t* part_begin;

@@ -715,6 +715,8 @@ struct pinot_amd_result {
   bool partitioned = false;
   JitKernel* jit_atomic = nullptr;  // partitioned plans: direct-atomic scan used when few docs match
   int atomic_grid = 1;
+  JitKernel* jit_sample = nullptr;  // partitioned plans: match count over every sample_stride-th tile
+  int sample_grid = 1;
   DevPartition part{};
   DevBuf hist, offs, part_begin, rec;
   int rec_bytes = 0, stage_cap = 0;
@@ -1061,7 +1063,7 @@ static int run_plan(pinot_amd_result* r) {
   HIP_OK(hipEventRecord(r->ev0, st));
   if (!r->inv_leaves.empty())
     HIP_OK(launch_expand_jobs(r->d_expand_jobs.p, (int32_t)r->inv_leaves.size(), r->expand_total, st));
-  HIP_OK(hipMemsetAsync(r->matched.p, 0, 8, st));
+  HIP_OK(hipMemsetAsync(r->matched.p, 0, 3 * sizeof(unsigned long long), st));
   if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
   if (r->jit && r->partitioned) {
     const DevSegment* segs = (const DevSegment*)r->d_segs.p;
@@ -1071,6 +1073,11 @@ static int run_plan(pinot_amd_result* r) {
     void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
     const unsigned pt = (unsigned)(kBlock * kPartSub);
     const unsigned count_grid = (unsigned)(r->grid * kPartCountRatio);
+    if (r->jit_sample) {
+      unsigned long long* sampled = matched + 1;
+      void* sargs[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&sampled, (void*)&r->part};
+      HIP_OK(hipModuleLaunchKernel(r->jit_sample->fn, (unsigned)r->sample_grid, 1, 1, kBlock, 1, 1, 0, st, sargs, nullptr));
+    }
     HIP_OK(hipModuleLaunchKernel(r->jit->fn, count_grid, 1, 1, pt, 1, 1, (unsigned)r->shmem, st, args, nullptr));
     HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, count_grid, r->part.offs, r->part.part_begin, st));
     if (r->jit_atomic)
@@ -1375,7 +1382,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * num_keys * 8);
   if (rc) return rc;
-  rc = r->matched.alloc(8);
+  rc = r->matched.alloc(3 * sizeof(unsigned long long));
   if (rc) return rc;
 
   // query-specialised kernel (hipRTC): needs every slot's encoding to agree across the batch
@@ -1514,6 +1521,20 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       for (auto* s : segs) docs += s->num_docs;
       r->part.atomic_threshold = r->jit_atomic ? docs / 64 : -1;
       if (ag && strcmp(ag, "force") == 0 && r->jit_atomic) r->part.atomic_threshold = INT64_MAX;
+      // selectivity sample: the filter over every 32nd tile (~3% of the filter columns' bytes); when
+      // the extrapolated matches fall under the threshold the count pass steps aside and the
+      // direct-atomic scan is the only full pass (a misestimate costs time, never correctness)
+      const char* sp = getenv("PINOT_AMD_SAMPLE_STRIDE");
+      const int64_t stride = sp ? atoll(sp) : 32;
+      if (r->jit_atomic && stride > 0 && tiles >= 64 * stride) {
+        JitPlan js = ja;
+        js.atomic_gate = false;
+        js.sample = true;
+        js.aggregate = false;
+        std::string err;
+        r->jit_sample = jit_get(js, &err);
+        if (r->jit_sample) r->part.sample_stride = stride;
+      }
       r->partitioned = true;
       r->part.nparts = jp.nparts;
       r->part.key_shift = jp.key_shift;
@@ -1556,6 +1577,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         nt = 1;
       r->atomic_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nt, tiles));
     }
+    if (r->jit_sample) {
+      int ns = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, r->jit_sample->fn, kBlock, 0) != hipSuccess || ns < 1)
+        ns = 1;
+      const int64_t vt = (tiles + r->part.sample_stride - 1) / r->part.sample_stride;
+      // a few tiles per wave: the sample is latency-bound, not bandwidth-bound
+      r->sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
+    }
+    r->part.counts = (unsigned long long*)r->matched.p;
   } else if (r->jit) {
     int nb = 0;
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock * r->scan_nsub, r->shmem) !=
@@ -1623,8 +1653,12 @@ int pinot_amd_result_destroy(pinot_amd_result* r) {
 
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_docs_matched: bad arguments");
-  HIP_OK(hipMemcpyAsync(h_out, r->matched.p, 8, hipMemcpyDeviceToHost, r->stream));
+  unsigned long long c[3];
+  HIP_OK(hipMemcpyAsync(c, r->matched.p, sizeof(c), hipMemcpyDeviceToHost, r->stream));
   HIP_OK(hipStreamSynchronize(r->stream));
+  // partitioned plans: the count pass (skipped when the sample hands over) and the direct-atomic scan
+  // (skipped when many docs match) both count every matching doc; whichever ran has the total
+  *h_out = (int64_t)std::max(c[0], c[2]);
   return 0;
 }
 

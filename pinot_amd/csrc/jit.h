@@ -59,6 +59,7 @@ struct JitPlan {
   // direct-atomic scan paired with a partitioned plan: runs only when the count pass found at most
   // part.atomic_threshold matching docs (then scatter + agg exit at once); counts no docs itself
   bool atomic_gate = false;
+  bool sample = false;  // match count over every part.sample_stride-th tile only (MODE_SAMPLE)
   // partitioned GROUP BY (DevPartition): count / scatter / LDS-aggregate kernels instead of one scan
   bool partitioned = false;
   int key_shift = 0;           // keys per partition = 2^key_shift

@@ -144,3 +144,33 @@ def test_wide_lds_table_plan(engine, monkeypatch, wide):
     nm, og = oracle.execute(q, bufs)
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("where", ["r_int < -995000", "r_int < 0", "ts = 25", "ts BETWEEN 10 AND 12 OR r_int > 999000"])
+@pytest.mark.parametrize("stride", [None, "0", "7"])
+def test_highcard_sampled_handover(engine, monkeypatch, where, stride):
+    """Partitioned plans over >= 64 x stride tiles first count the filter's matches on every
+    stride-th tile; an extrapolated count under docs/64 skips the count pass and leaves the batch to
+    the direct-atomic scan. Selective (0.25%), broad (50%) and docId-clustered (sorted `ts`) filters,
+    sampling off ("0") and a non-power-of-two stride: identical groups and matched-doc count."""
+    monkeypatch.setenv("PINOT_AMD_JIT", "1")
+    monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
+    monkeypatch.delenv("PINOT_AMD_ATOMIC_HANDOVER", raising=False)
+    if stride is None:
+        monkeypatch.delenv("PINOT_AMD_SAMPLE_STRIDE", raising=False)
+    else:
+        monkeypatch.setenv("PINOT_AMD_SAMPLE_STRIDE", stride)
+    rng = np.random.default_rng(31)
+    bufs = [random_segment(rng, 900_000 + 4099 * i, name=f"h{i}", bits_cards=(1000, 1000), sorted_col=True)
+            for i in range(3)]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = ("SET numGroupsLimit = 2000000; SELECT d0, d1, COUNT(*), SUM(r_int), MIN(r_long), MAX(r_double) FROM t "
+         f"WHERE {where} GROUP BY d0, d1")
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert res.kernel_info() == "jit-partitioned"
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
+    res.execute_again()
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
