@@ -1439,7 +1439,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       for (const JitSlot& js : jp.slots)
         bpr += js.enc == ENC_FIXED_BIT ? (js.bits > 0 ? js.bits : 16) / 8.0 : js.enc == ENC_RAW ? value_size(js.type) : 0.0;
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
-      if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(4, atoi(pd)));
+      if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
       if (const char* lr = getenv("PINOT_AMD_LANE_TABLES"))
         if (strcmp(lr, "0") == 0) {
           for (auto& js : jp.slots) js.dict_regs = 0;
