@@ -96,6 +96,11 @@ typedef struct pinot_amd_column_spec {
 } pinot_amd_column_spec;
 
 int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segment** out);
+/* Raw (no-dictionary) forward indexes may use any ChunkCompressionType (ChunkCompressionType.java:22):
+ * PASS_THROUGH chunks are copied; LZ4, LZ4_LENGTH_PREFIXED, SNAPPY, DELTA and DELTADELTA chunks are
+ * decoded on the device (one wave per chunk, BaseChunkForwardIndexReader.decompressChunk); ZSTANDARD
+ * and GZIP chunks are inflated on the host with the system libzstd / zlib. Malformed chunks fail
+ * with PINOT_AMD_EINVAL. */
 int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_spec* spec);
 int pinot_amd_segment_destroy(pinot_amd_segment* seg);
 int64_t pinot_amd_segment_num_docs(const pinot_amd_segment* seg);

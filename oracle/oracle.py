@@ -76,6 +76,10 @@ def lib():
         L.oracle_roaring_to_bitset.argtypes = [P, I64, P, I64]
         L.oracle_lz4_decompress.restype = I64
         L.oracle_lz4_decompress.argtypes = [P, I64, P, I64]
+        L.oracle_snappy_decompress.restype = I64
+        L.oracle_snappy_decompress.argtypes = [P, I64, P, I64]
+        L.oracle_delta_decompress.restype = I64
+        L.oracle_delta_decompress.argtypes = [P, I64, P, I64, C.c_int32]
         L.oracle_inverted_to_bitset.argtypes = [P, C.c_int32, P, C.c_int32, P, I64]
         L.oracle_filter.restype = I64
         L.oracle_filter.argtypes = [C.POINTER(OColumn), I64, C.POINTER(OLeaf), C.c_int32, P]
@@ -161,6 +165,29 @@ def _raw_range(col: ColumnBuffers, p):
     return lo, hi
 
 
+def decompress_chunk(comp: int, src: np.ndarray, dst: np.ndarray, want: int) -> int:
+    """ChunkDecompressor per ChunkCompressionType (ChunkCompressorFactory.getDecompressor):
+    LZ4 / SNAPPY / DELTA / DELTADELTA restated in pinot_oracle.c; ZSTANDARD (zstd-jni) through
+    pyarrow's bundled libzstd and GZIP (java.util.zip.Inflater, zlib stream + BE size) through
+    Python's zlib -- third-party entropy decoders used as-is by this checker."""
+    if comp in (3, 4):
+        return lib().oracle_lz4_decompress(src.ctypes.data, src.size, dst.ctypes.data, want)
+    if comp == 1:
+        return lib().oracle_snappy_decompress(src.ctypes.data, src.size, dst.ctypes.data, want)
+    if comp in (6, 7):
+        return lib().oracle_delta_decompress(src.ctypes.data, src.size, dst.ctypes.data, want, int(comp == 7))
+    if comp == 2:
+        import pyarrow as pa
+        raw = pa.Codec("zstd").decompress(src.tobytes(), decompressed_size=want, asbytes=True)
+    elif comp == 5:
+        import zlib
+        raw = zlib.decompress(src[:-4].tobytes())
+    else:
+        raise NotImplementedError(comp)
+    dst[:len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+    return len(raw)
+
+
 def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
     """The contiguous big-endian values of a raw forward index: the data region of PASS_THROUGH
     chunks, or the LZ4 / LZ4_LENGTH_PREFIXED chunks decoded one by one
@@ -169,7 +196,7 @@ def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
     fb = np.frombuffer(cb.fwd, dtype=np.uint8)
     if h.compression == 0:
         return fb[h.raw_data_start:].copy()
-    assert h.compression in (3, 4), h.compression
+    assert h.compression in range(1, 8), h.compression
     off_size = 4 if h.version <= 2 else 8
     offs = np.frombuffer(cb.fwd, dtype=">i4" if off_size == 4 else ">i8", count=h.num_chunks,
                          offset=h.data_header_start).astype(np.int64)
@@ -180,8 +207,8 @@ def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
     for s, e in zip(offs, ends):
         src = fb[s + (4 if h.compression == 4 else 0):e].copy()
         want = min(h.docs_per_chunk * h.size_of_entry, total - pos)
-        got = lib().oracle_lz4_decompress(src.ctypes.data, src.size, out[pos:].ctypes.data, want)
-        assert got == want, (got, want)
+        got = decompress_chunk(h.compression, src, out[pos:], want)
+        assert got == want, (h.compression, got, want)
         pos += want
     return out
 

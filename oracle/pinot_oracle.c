@@ -197,6 +197,100 @@ int64_t oracle_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64
   return op;
 }
 
+/* Snappy raw block decoding (org.xerial.snappy:snappy-java 1.1.10.x, third-party: Snappy.uncompress,
+ * the chunk decompressor behind ChunkCompressionType.SNAPPY, pinot-segment-local/.../io/compression/
+ * SnappyDecompressor.java:40-44), restated from the published format: a varint uncompressed length,
+ * then tagged elements -- 00 literal (length-1 in the tag's upper 6 bits, or 1-4 LE bytes after it
+ * for 60..63), 01 copy (length 4..11, 11-bit offset), 10 copy (length 1..64, LE16 offset),
+ * 11 copy (length 1..64, LE32 offset). Returns bytes written or -1. */
+int64_t oracle_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+  int64_t ip = 0, op = 0;
+  uint64_t len = 0;
+  for (int sh = 0;; sh += 7) {
+    if (ip >= n || sh > 28) return -1;
+    uint32_t b = src[ip++];
+    len |= (uint64_t)(b & 0x7F) << sh;
+    if (!(b & 0x80)) break;
+  }
+  if ((int64_t)len > cap) return -1;
+  while (ip < n) {
+    uint32_t tag = src[ip++];
+    int64_t l, off;
+    if ((tag & 3) == 0) {
+      l = (tag >> 2) + 1;
+      if (l > 60) {
+        int nb = (int)l - 60;
+        if (ip + nb > n) return -1;
+        l = 0;
+        for (int k = 0; k < nb; k++) l |= (int64_t)src[ip + k] << (8 * k);
+        l += 1;
+        ip += nb;
+      }
+      if (ip + l > n || op + l > (int64_t)len) return -1;
+      for (int64_t k = 0; k < l; k++) dst[op++] = src[ip++];
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (ip + 1 > n) return -1;
+      l = 4 + ((tag >> 2) & 7);
+      off = ((int64_t)(tag >> 5) << 8) | src[ip];
+      ip += 1;
+    } else if ((tag & 3) == 2) {
+      if (ip + 2 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = src[ip] | (src[ip + 1] << 8);
+      ip += 2;
+    } else {
+      if (ip + 4 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = (int64_t)le32(src + ip);
+      ip += 4;
+    }
+    if (off == 0 || off > op || op + l > (int64_t)len) return -1;
+    for (int64_t k = 0; k < l; k++, op++) dst[op] = dst[op - off];
+  }
+  return op == (int64_t)len ? op : -1;
+}
+
+static uint64_t rd_be(const uint8_t* p, int w) {
+  uint64_t v = 0;
+  for (int k = 0; k < w; k++) v = (v << 8) | p[k];
+  return v;
+}
+static void wr_be(uint8_t* p, int w, uint64_t v) {
+  for (int k = w - 1; k >= 0; k--, v >>= 8) p[k] = (uint8_t)v;
+}
+
+/* DELTA (dd = 0) / DELTADELTA (dd = 1) chunks (DeltaDecompressor.java:45-130,
+ * DeltaDeltaDecompressor.java:45-140): flag byte (1 = LONG values, else INT), BE count, BE first
+ * value, BE compressed size, then an LZ4 block of BE deltas (DELTADELTA: the first delta, then
+ * deltas of deltas); values are rebuilt with Java's wrapping int/long arithmetic. */
+int64_t oracle_delta_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t dd) {
+  if (n < 5) return -1;
+  const int w = src[0] == 1 ? 8 : 4;
+  const int64_t cnt = (int32_t)rd_be(src + 1, 4);
+  if (cnt < 0 || cnt * w > cap) return -1;
+  if (cnt == 0) return 0;
+  if (n < 5 + w) return -1;
+  uint64_t prev = rd_be(src + 5, w);
+  wr_be(dst, w, prev);
+  if (cnt == 1) return w;
+  if (n < 9 + w) return -1;
+  const int64_t cs = (int32_t)rd_be(src + 5 + w, 4);
+  if (cs < 0 || 9 + w + cs > n) return -1;
+  const int64_t got = oracle_lz4_decompress(src + 9 + w, cs, dst + w, (cnt - 1) * w);
+  if (got != (cnt - 1) * w) return -1;
+  const uint64_t mask = w == 8 ? ~0ull : 0xFFFFFFFFull;
+  uint64_t delta = 0;
+  for (int64_t i = 1; i < cnt; i++) {
+    const uint64_t e = rd_be(dst + i * w, w);
+    delta = (dd && i > 1) ? (delta + e) & mask : e;
+    prev = (prev + delta) & mask;
+    wr_be(dst + i * w, w, prev);
+  }
+  return cnt * w;
+}
+
 /* ------------------------------------------------------------------ roaring */
 
 /* RoaringBitmap 1.6.14 portable deserialisation (org.roaringbitmap.buffer.ImmutableRoaringBitmap,

@@ -78,6 +78,8 @@ double oracle_raw_read_f64(const uint8_t* raw, int32_t type, int64_t index);
 void oracle_column_dict_ids(const oracle_column* col, int64_t start, int64_t n, int32_t* out);
 
 int64_t oracle_lz4_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+int64_t oracle_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
+int64_t oracle_delta_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int32_t dd);
 
 /* ---- inverted index (BitmapInvertedIndexReader + RoaringBitmap portable format) ---- */
 int oracle_roaring_to_bitset(const uint8_t* buf, int64_t len, uint64_t* bitset, int64_t num_docs);

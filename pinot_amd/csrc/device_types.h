@@ -97,6 +97,16 @@ struct ExpandJob {
   int32_t nsel, nchunks;
 };
 
+// One compressed chunk of a raw forward index (BaseChunkForwardIndexWriter layout), decoded on the
+// device at staging by one wave. codec: ChunkCompressionType (1 SNAPPY, 3 LZ4 -- the 4-byte length
+// prefix of LZ4_LENGTH_PREFIXED already skipped by the host --, 6 DELTA, 7 DELTADELTA).
+struct ChunkJob {
+  uint64_t src_off;  // into the staged compressed file
+  uint64_t dst_off;  // into the contiguous decoded values
+  uint32_t src_len, dst_len;
+  int32_t codec, pad;
+};
+
 // Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the
 // kernel's per-slot loop indexes the decoded values with compile-time indices only.
 struct DevQuery {
@@ -108,7 +118,7 @@ struct DevQuery {
   int32_t nacc;                             // accumulator arrays, acc 0 = COUNT
   int32_t acc_op[kMaxAcc];
   int32_t lds_keys;                         // > 0: LDS-privatised table of lds_keys keys
-  int32_t pad0;
+  int32_t agg_only;                         // no GROUP BY: MIN/MAX propagate NaN (Math.min/max)
   int64_t num_keys;                         // dense key space (1 for aggregation only)
   int64_t total_tiles;
 };

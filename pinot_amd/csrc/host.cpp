@@ -1,6 +1,7 @@
 // host.cpp — host side of libpinot_amd.so: segment staging into HBM, per-segment predicate
 // resolution (PredicateEvaluatorProvider), query planning for the fused scan kernel, execution
 // over a batch of segments and result extraction. Implements include/pinot_amd.h.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,6 +30,8 @@ hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, 
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
 hipError_t launch_read_raw(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out, hipStream_t st);
+hipError_t launch_chunk_decompress(const uint8_t* src, uint8_t* dst, const void* jobs, int32_t njobs, int32_t* status,
+                                   hipStream_t st);
 hipError_t launch_bitset_binop(const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n, int op,
                                hipStream_t st);
 hipError_t launch_bitset_not(const uint64_t* a, uint64_t* out, int64_t num_docs, hipStream_t st);
@@ -125,46 +128,6 @@ static std::u16string to_utf16(const std::string& s) {
   return out;
 }
 static bool java_less(const std::string& a, const std::string& b) { return to_utf16(a) < to_utf16(b); }
-
-// LZ4 block decompression (lz4-java fastCompressor output, used by Pinot's LZ4 / LZ4_LENGTH_PREFIXED
-// chunk compressors: pinot-segment-local/.../io/compression/LZ4Decompressor.java). Returns the number
-// of bytes written or -1 on a malformed block.
-static int64_t lz4_block_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap) {
-  size_t ip = 0, op = 0;
-  while (ip < n) {
-    const uint32_t token = src[ip++];
-    size_t lit = token >> 4;
-    if (lit == 15) {
-      uint8_t b;
-      do {
-        if (ip >= n) return -1;
-        b = src[ip++];
-        lit += b;
-      } while (b == 255);
-    }
-    if (ip + lit > n || op + lit > cap) return -1;
-    memcpy(dst + op, src + ip, lit);
-    ip += lit;
-    op += lit;
-    if (ip >= n) break;  // last sequence: literals only
-    if (ip + 2 > n) return -1;
-    const size_t off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
-    ip += 2;
-    size_t ml = token & 15;
-    if (ml == 15) {
-      uint8_t b;
-      do {
-        if (ip >= n) return -1;
-        b = src[ip++];
-        ml += b;
-      } while (b == 255);
-    }
-    ml += 4;
-    if (off == 0 || off > op || op + ml > cap) return -1;
-    for (size_t k = 0; k < ml; ++k, ++op) dst[op] = dst[op - off];  // overlapping copies are byte-serial
-  }
-  return (int64_t)op;
-}
 
 struct RoaringContainerHost {
   uint32_t key, kind, count, pad;
@@ -318,6 +281,101 @@ static int build_inverted_directory(Column& c, const uint8_t* inv, size_t n) {
   return 0;
 }
 
+// ZSTANDARD / GZIP chunks are entropy-coded (FSE/Huffman) streams with no intra-chunk parallelism
+// worth a wave: they are inflated on the host at staging with the system's libzstd / zlib (the
+// libraries zstd-jni and java.util.zip wrap), loaded on first use.
+struct HostCodecs {
+  size_t (*zstd_decompress)(void*, size_t, const void*, size_t) = nullptr;
+  unsigned (*zstd_is_error)(size_t) = nullptr;
+  int (*z_uncompress)(uint8_t*, unsigned long*, const uint8_t*, unsigned long) = nullptr;
+  HostCodecs() {
+    if (void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      zstd_decompress = (decltype(zstd_decompress))dlsym(h, "ZSTD_decompress");
+      zstd_is_error = (decltype(zstd_is_error))dlsym(h, "ZSTD_isError");
+    }
+    if (void* h = dlopen("libz.so.1", RTLD_NOW | RTLD_LOCAL)) z_uncompress = (decltype(z_uncompress))dlsym(h, "uncompress");
+  }
+};
+static const HostCodecs& host_codecs() {
+  static HostCodecs hc;
+  return hc;
+}
+
+// Stage a raw forward index with compressed chunks (BaseChunkForwardIndexReader.java:60-105,150-185;
+// codecs per ChunkCompressionType.java:22): LZ4, LZ4_LENGTH_PREFIXED, SNAPPY, DELTA and DELTADELTA
+// chunks are decoded on the device (chunk_decompress_kernel, one wave per chunk) straight into the
+// column's HBM buffer; ZSTANDARD and GZIP on the host.
+static int stage_compressed_chunks(Column& c, const pinot_amd_column_spec* spec, const uint8_t* fwd, int32_t version,
+                                   int32_t num_chunks, int32_t size, int32_t comp, int32_t dhs, size_t need) {
+  const int32_t dpc = (int32_t)be32(fwd + 8);
+  const size_t off_size = version <= 2 ? 4 : 8;
+  if (dpc <= 0 || num_chunks < 0 || (size_t)dhs + (size_t)num_chunks * off_size > spec->fwd_size)
+    return fail(PINOT_AMD_EINVAL, "column %s: bad chunk header", spec->name);
+  if (comp < 1 || comp > 7) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d", spec->name, comp);
+  if ((comp == 6 || comp == 7) && is_float(c.type))
+    return fail(PINOT_AMD_EINVAL, "column %s: DELTA chunks on a floating-point column", spec->name);
+  std::vector<ChunkJob> jobs;
+  size_t op = 0;
+  for (int32_t ch = 0; ch < num_chunks && op < need; ++ch) {
+    const uint8_t* o = fwd + dhs + (size_t)ch * off_size;
+    const uint64_t start = off_size == 4 ? be32(o) : be64(o);
+    const uint64_t end = ch + 1 < num_chunks ? (off_size == 4 ? be32(o + 4) : be64(o + 8)) : spec->fwd_size;
+    if (start > end || end > spec->fwd_size) return fail(PINOT_AMD_EINVAL, "column %s: bad chunk offsets", spec->name);
+    ChunkJob j{};
+    j.src_off = start;
+    j.src_len = (uint32_t)(end - start);
+    j.dst_off = op;
+    j.dst_len = (uint32_t)std::min<size_t>((size_t)dpc * size, need - op);
+    j.codec = comp == 4 ? 3 : comp;
+    if (comp == 4) {  // LZ4CompressorWithLength: 4-byte LE decompressed length first
+      if (j.src_len < 4) return fail(PINOT_AMD_EINVAL, "column %s: truncated LZ4 chunk %d", spec->name, ch);
+      j.src_off += 4;
+      j.src_len -= 4;
+    }
+    jobs.push_back(j);
+    op += j.dst_len;
+  }
+  if (op != need) return fail(PINOT_AMD_EINVAL, "column %s: chunks hold %zu of %zu bytes", spec->name, op, need);
+  if (jobs.empty()) return c.fwd.alloc_copy(nullptr, 0, kPadBytes);
+  if (comp == 2 || comp == 5) {
+    const HostCodecs& hc = host_codecs();
+    if (comp == 2 ? !hc.zstd_decompress || !hc.zstd_is_error : !hc.z_uncompress)
+      return fail(PINOT_AMD_EUNSUPPORTED, "column %s: %s not loadable for chunk compression %d", spec->name,
+                  comp == 2 ? "libzstd.so.1" : "libz.so.1", comp);
+    std::vector<uint8_t> out(need);
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      const ChunkJob& j = jobs[k];
+      size_t got;
+      if (comp == 2) {
+        got = hc.zstd_decompress(out.data() + j.dst_off, j.dst_len, fwd + j.src_off, j.src_len);
+        if (hc.zstd_is_error(got)) got = (size_t)-1;
+      } else {  // GzipCompressor: zlib stream, then the BE uncompressed size
+        unsigned long dl = j.dst_len;
+        got = j.src_len >= 4 && hc.z_uncompress(out.data() + j.dst_off, &dl, fwd + j.src_off, j.src_len - 4) == 0
+                  ? (size_t)dl : (size_t)-1;
+      }
+      if (got != j.dst_len)
+        return fail(PINOT_AMD_EINVAL, "column %s: chunk %zu of compression %d decoded to %lld of %u bytes", spec->name,
+                    k, comp, (long long)(int64_t)got, j.dst_len);
+    }
+    return c.fwd.alloc_copy(out.data(), need, kPadBytes);
+  }
+  DevBuf d_src, d_jobs, d_status;
+  int rc = d_src.alloc_copy(fwd, spec->fwd_size, 64);
+  if (!rc) rc = d_jobs.alloc_copy(jobs.data(), jobs.size() * sizeof(ChunkJob), 0);
+  if (!rc) rc = d_status.alloc_copy(nullptr, 0, jobs.size() * 4);
+  if (!rc) rc = c.fwd.alloc_copy(nullptr, 0, need + kPadBytes);
+  if (rc) return rc;
+  HIP_OK(launch_chunk_decompress((const uint8_t*)d_src.p, (uint8_t*)c.fwd.p, d_jobs.p, (int32_t)jobs.size(),
+                                 (int32_t*)d_status.p, nullptr));
+  HIP_OK(hipDeviceSynchronize());
+  std::vector<int32_t> st(jobs.size());
+  HIP_OK(hipMemcpy(st.data(), d_status.p, st.size() * 4, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < st.size(); ++k)
+    if (st[k]) return fail(PINOT_AMD_EINVAL, "column %s: chunk %zu (compression %d) is malformed", spec->name, k, comp);
+  return 0;
+}
+
 extern "C" {
 
 int pinot_amd_abi_version(void) { return PINOT_AMD_ABI_VERSION; }
@@ -401,35 +459,9 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
       if (comp == 0) {  // PASS_THROUGH: chunks are contiguous raw values
         if (spec->fwd_size < raw_start + need) return fail(PINOT_AMD_EINVAL, "column %s: raw data truncated", spec->name);
         rc = c->fwd.alloc_copy(fwd + raw_start, need, kPadBytes);
-      } else if (comp == 3 || comp == 4) {
-        // LZ4 / LZ4_LENGTH_PREFIXED chunks: decompressed once while staging, kept as contiguous values in HBM
-        const int32_t dpc = (int32_t)be32(fwd + 8);
-        std::vector<uint8_t> out(need + 16);
-        size_t op = 0;
-        for (int32_t ch = 0; ch < num_chunks; ++ch) {
-          const uint8_t* o = fwd + dhs + (size_t)ch * off_size;
-          const uint64_t start = off_size == 4 ? be32(o) : be64(o);
-          const uint64_t end = ch + 1 < num_chunks ? (off_size == 4 ? be32(o + 4) : be64(o + 8)) : spec->fwd_size;
-          if (start > end || end > spec->fwd_size) return fail(PINOT_AMD_EINVAL, "column %s: bad chunk offsets", spec->name);
-          const uint8_t* src = fwd + start;
-          size_t len = (size_t)(end - start);
-          if (comp == 4) {  // LZ4CompressorWithLength: 4-byte LE decompressed length first
-            if (len < 4) return fail(PINOT_AMD_EINVAL, "column %s: truncated LZ4 chunk", spec->name);
-            src += 4;
-            len -= 4;
-          }
-          const size_t want = std::min<size_t>((size_t)dpc * size, need - op);
-          const int64_t got = lz4_block_decompress(src, len, out.data() + op, want);
-          if (got != (int64_t)want)
-            return fail(PINOT_AMD_EINVAL, "column %s: LZ4 chunk %d decompressed to %lld of %zu bytes", spec->name, ch,
-                        (long long)got, want);
-          op += want;
-        }
-        if (op != need) return fail(PINOT_AMD_EINVAL, "column %s: decompressed %zu of %zu bytes", spec->name, op, need);
-        rc = c->fwd.alloc_copy(out.data(), need, kPadBytes);
       } else {
-        return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d (PASS_THROUGH, LZ4 staged)", spec->name,
-                    comp);
+        // compressed chunks: decoded once while staging, kept as contiguous values in HBM
+        rc = stage_compressed_chunks(*c, spec, fwd, version, num_chunks, size, comp, dhs, need);
       }
       break;
     }
@@ -1289,6 +1321,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   for (size_t j = 0; j < Q.group_by.size(); ++j) q.slot_group_stride[slot_of(Q.group_by[j])] = r->key_stride[j];
   if (Q.aggs.empty() && Q.group_by.empty()) q.nacc = 0;  // filter-only: count matches
+  q.agg_only = Q.group_by.empty() ? 1 : 0;
 
   // LDS-privatised table when it fits in 40 KB (keeps >= 4 blocks of 256 threads per CU)
   const int64_t lds_bytes = (int64_t)q.nacc * num_keys * 8;

@@ -433,8 +433,10 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
                 const double d = slot_value_f64(col, v[sl][k]);
-                const uint64_t o = ordered_from_double(d);
-                if (((match >> k) & 1) && d == d && o < p) p = o;
+                // NaN: skipped by the group-by `value < min`, ordered below everything (decodes
+                // back to NaN) for aggregation-only Math.min
+                const uint64_t o = d == d ? ordered_from_double(d) : q.agg_only ? 0ull : ~0ull;
+                if (((match >> k) & 1) && o < p) p = o;
               }
               r = wave_min_u64(p);
             } else {
@@ -442,8 +444,8 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
                 const double d = slot_value_f64(col, v[sl][k]);
-                const uint64_t o = ordered_from_double(d);
-                if (((match >> k) & 1) && d == d && o > p) p = o;
+                const uint64_t o = d == d ? ordered_from_double(d) : q.agg_only ? ~0ull : 0ull;
+                if (((match >> k) & 1) && o > p) p = o;
               }
               r = wave_max_u64(p);
             }
@@ -468,8 +470,12 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restri
                   r = (uint64_t)slot_value_i64(col, v[sl][k]);
                 } else {
                   const double d = slot_value_f64(col, v[sl][k]);
-                  if (op != ACC_SUM_F64 && d != d) continue;  // MIN/MAX skip NaN (`value < min`)
-                  r = op == ACC_SUM_F64 ? (uint64_t)__double_as_longlong(d) : ordered_from_double(d);
+                  if (op != ACC_SUM_F64 && d != d) {
+                    if (!q.agg_only) continue;  // group-by MIN/MAX skip NaN (`value < min`)
+                    r = op == ACC_MIN ? 0ull : ~0ull;  // Math.min/max propagate NaN
+                  } else {
+                    r = op == ACC_SUM_F64 ? (uint64_t)__double_as_longlong(d) : ordered_from_double(d);
+                  }
                 }
                 acc_apply(op, row + (int64_t)a * tstride, r);
               }
@@ -789,6 +795,216 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
 static inline unsigned grid_for(int64_t n, int per_block) {
   int64_t g = (n + per_block - 1) / per_block;
   return (unsigned)(g < 1 ? 1 : g);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Raw-chunk decompression at staging (BaseChunkForwardIndexReader.decompressChunk,
+// BaseChunkForwardIndexReader.java:150-185, with the codecs of io/compression/*Decompressor.java).
+// One wave per chunk: the (sequential) token stream is parsed wave-uniformly, every literal run and
+// match is copied by all 64 lanes. A match with offset < length repeats the `off` bytes before it,
+// so byte i of the match is dst[op - off + i % off] -- no byte-serial copy. Stores of one step become
+// visible to the wave's later loads through a workgroup-scope fence (the block is one wave).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+__device__ __forceinline__ void wave_match_copy(uint8_t* dst, int64_t op, int64_t off, int64_t ml, int lane) {
+  if (off >= ml) {
+    for (int64_t i = lane; i < ml; i += 64) dst[op + i] = dst[op - off + i];
+  } else {
+    for (int64_t i = lane; i < ml; i += 64) dst[op + i] = dst[op - off + i % off];
+  }
+}
+
+// LZ4 block (lz4-java LZ4SafeDecompressor semantics); returns bytes written or -1
+__device__ int64_t wave_lz4(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int lane) {
+  int64_t ip = 0, op = 0;
+  while (ip < n) {
+    const uint32_t token = src[ip++];
+    int64_t lit = token >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (ip + lit > n || op + lit > cap) return -1;
+    for (int64_t i = lane; i < lit; i += 64) dst[op + i] = src[ip + i];
+    ip += lit;
+    op += lit;
+    if (ip >= n) break;  // last sequence: literals only
+    if (ip + 2 > n) return -1;
+    const int64_t off = (int64_t)src[ip] | ((int64_t)src[ip + 1] << 8);
+    ip += 2;
+    int64_t ml = token & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (off == 0 || off > op || op + ml > cap) return -1;
+    wave_fence();
+    wave_match_copy(dst, op, off, ml, lane);
+    wave_fence();
+    op += ml;
+  }
+  return op;
+}
+
+// Snappy raw block (snappy-java Snappy.uncompress); returns bytes written or -1
+__device__ int64_t wave_snappy(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int lane) {
+  int64_t ip = 0, op = 0;
+  uint64_t len = 0;
+  for (int sh = 0;; sh += 7) {
+    if (ip >= n || sh > 28) return -1;
+    const uint32_t b = src[ip++];
+    len |= (uint64_t)(b & 0x7F) << sh;
+    if (!(b & 0x80)) break;
+  }
+  if ((int64_t)len > cap) return -1;
+  while (ip < n) {
+    const uint32_t tag = src[ip++];
+    int64_t l, off;
+    if ((tag & 3) == 0) {
+      l = (tag >> 2) + 1;
+      if (l > 60) {
+        const int nb = (int)l - 60;
+        if (ip + nb > n) return -1;
+        l = 0;
+        for (int k = 0; k < nb; ++k) l |= (int64_t)src[ip + k] << (8 * k);
+        l += 1;
+        ip += nb;
+      }
+      if (ip + l > n || op + l > (int64_t)len) return -1;
+      for (int64_t i = lane; i < l; i += 64) dst[op + i] = src[ip + i];
+      ip += l;
+      op += l;
+      continue;
+    }
+    if ((tag & 3) == 1) {
+      if (ip + 1 > n) return -1;
+      l = 4 + ((tag >> 2) & 7);
+      off = ((int64_t)(tag >> 5) << 8) | src[ip];
+      ip += 1;
+    } else if ((tag & 3) == 2) {
+      if (ip + 2 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = (int64_t)src[ip] | ((int64_t)src[ip + 1] << 8);
+      ip += 2;
+    } else {
+      if (ip + 4 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = (int64_t)((uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8) | ((uint32_t)src[ip + 2] << 16) |
+                      ((uint32_t)src[ip + 3] << 24));
+      ip += 4;
+    }
+    if (off == 0 || off > op || op + l > (int64_t)len) return -1;
+    wave_fence();
+    wave_match_copy(dst, op, off, l, lane);
+    wave_fence();
+    op += l;
+  }
+  return op == (int64_t)len ? op : -1;
+}
+
+// inclusive prefix sum (Java wrapping arithmetic) over the W-byte big-endian values v[first..cnt)
+template <typename U>
+__device__ void wave_prefix_be(uint8_t* v, int64_t first, int64_t cnt, int lane) {
+  U carry = 0;
+  for (int64_t base = first; base < cnt; base += 64) {
+    const int64_t i = base + lane;
+    U x = 0;
+    if (i < cnt) {
+      // 4-byte accesses only: a chunk of an INT column may use the 8-byte layout at a 4-aligned offset
+      const uint32_t* q = (const uint32_t*)(v + i * sizeof(U));
+      if constexpr (sizeof(U) == 4) x = __builtin_bswap32(q[0]);
+      else x = ((uint64_t)__builtin_bswap32(q[0]) << 32) | __builtin_bswap32(q[1]);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const U y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    x += carry;
+    if (i < cnt) {
+      uint32_t* q = (uint32_t*)(v + i * sizeof(U));
+      if constexpr (sizeof(U) == 4) {
+        q[0] = __builtin_bswap32(x);
+      } else {
+        q[0] = __builtin_bswap32((uint32_t)(x >> 32));
+        q[1] = __builtin_bswap32((uint32_t)x);
+      }
+    }
+    carry = __shfl(x, 63, 64);
+  }
+}
+
+// DELTA / DELTADELTA chunk (DeltaDecompressor.java, DeltaDeltaDecompressor.java): flag byte
+// (1 = LONG layout), BE count, BE first value, BE LZ4 size, LZ4 block of BE (delta-of-)deltas
+__device__ int64_t wave_delta(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, bool dd, int lane) {
+  if (n < 5) return -1;
+  const int w = src[0] == 1 ? 8 : 4;
+  const int64_t cnt = (int32_t)(((uint32_t)src[1] << 24) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 8) | src[4]);
+  if (cnt < 0 || cnt * w > cap) return -1;
+  if (cnt == 0) return 0;
+  if (n < 5 + w) return -1;
+  for (int i = lane; i < w; i += 64) dst[i] = src[5 + i];  // first value, as stored
+  if (cnt == 1) return w;
+  if (n < 9 + w) return -1;
+  const uint8_t* p = src + 5 + w;
+  const int64_t cs = (int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]);
+  if (cs < 0 || 9 + w + cs > n) return -1;
+  if (wave_lz4(p + 4, cs, dst + w, (cnt - 1) * w, lane) != (cnt - 1) * w) return -1;
+  wave_fence();
+  if (w == 8) {
+    if (dd) {
+      wave_prefix_be<uint64_t>(dst, 1, cnt, lane);
+      wave_fence();
+    }
+    wave_prefix_be<uint64_t>(dst, 0, cnt, lane);
+  } else {
+    if (dd) {
+      wave_prefix_be<uint32_t>(dst, 1, cnt, lane);
+      wave_fence();
+    }
+    wave_prefix_be<uint32_t>(dst, 0, cnt, lane);
+  }
+  return cnt * w;
+}
+
+// status[j]: 0 decoded to exactly dst_len bytes, 1 malformed or wrong size, 2 unknown codec
+__global__ void __launch_bounds__(64) chunk_decompress_kernel(const uint8_t* __restrict__ src, uint8_t* dst,
+                                                              const ChunkJob* __restrict__ jobs, int32_t njobs,
+                                                              int32_t* __restrict__ status) {
+  const int lane = threadIdx.x;
+  for (int32_t j = blockIdx.x; j < njobs; j += gridDim.x) {
+    const ChunkJob jb = jobs[j];
+    const uint8_t* s = src + jb.src_off;
+    uint8_t* d = dst + jb.dst_off;
+    int64_t got;
+    switch (jb.codec) {
+      case 1: got = wave_snappy(s, jb.src_len, d, jb.dst_len, lane); break;
+      case 3: got = wave_lz4(s, jb.src_len, d, jb.dst_len, lane); break;
+      case 6: got = wave_delta(s, jb.src_len, d, jb.dst_len, false, lane); break;
+      case 7: got = wave_delta(s, jb.src_len, d, jb.dst_len, true, lane); break;
+      default: got = -2;
+    }
+    if (lane == 0) status[j] = got == (int64_t)jb.dst_len ? 0 : got == -2 ? 2 : 1;
+  }
+}
+
+hipError_t launch_chunk_decompress(const uint8_t* src, uint8_t* dst, const void* jobs, int32_t njobs, int32_t* status,
+                                   hipStream_t st) {
+  if (njobs <= 0) return hipSuccess;
+  const int grid = njobs < 65536 ? njobs : 65536;
+  hipLaunchKernelGGL(chunk_decompress_kernel, dim3(grid), dim3(64), 0, st, src, dst, (const ChunkJob*)jobs, njobs,
+                     status);
+  return hipGetLastError();
 }
 
 template <int NS>

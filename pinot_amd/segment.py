@@ -45,8 +45,13 @@ VALUE_SIZE = {INT: 4, LONG: 8, FLOAT: 4, DOUBLE: 8}
 
 # ChunkCompressionType (pinot-segment-spi/.../compression/ChunkCompressionType.java:22)
 PASS_THROUGH = 0
+SNAPPY = 1
+ZSTANDARD = 2
 LZ4 = 3
 LZ4_LENGTH_PREFIXED = 4
+GZIP = 5
+DELTA = 6
+DELTADELTA = 7
 
 # Default null values (FieldSpec.DEFAULT_*_NULL_VALUE_OF_*), used when ingesting nulls
 DEFAULT_DIMENSION_NULL = {INT: np.iinfo(np.int32).min, LONG: np.iinfo(np.int64).min,
@@ -175,8 +180,10 @@ def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_p
     data = np.ascontiguousarray(values).astype(_NP_BE[stored_type]).tobytes()
     if compression == PASS_THROUGH:
         return raw_fwd_header(int(values.size), stored_type, version, docs_per_chunk) + data
-    if compression not in (LZ4, LZ4_LENGTH_PREFIXED):
+    if compression not in (SNAPPY, ZSTANDARD, LZ4, LZ4_LENGTH_PREFIXED, GZIP, DELTA, DELTADELTA):
         raise NotImplementedError(f"compression {compression}")
+    if compression in (DELTA, DELTADELTA) and stored_type not in (INT, LONG):
+        raise ValueError("DELTA / DELTADELTA chunks hold INT or LONG values")
     # compressed chunks (BaseChunkForwardIndexWriter.writeChunk): offsets point at each compressed chunk
     if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
         docs_per_chunk = 1 << (docs_per_chunk - 1).bit_length()
@@ -186,10 +193,7 @@ def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_p
     chunks = []
     for c in range(0, len(data), chunk_bytes):
         raw = data[c:c + chunk_bytes]
-        blk = lz4_block_compress(raw)
-        if compression == LZ4_LENGTH_PREFIXED:  # LZ4CompressorWithLength: decompressed length, LE int
-            blk = struct.pack("<i", len(raw)) + blk
-        chunks.append(blk)
+        chunks.append(chunk_compress(raw, compression))
     num_chunks = len(chunks)
     off_size = 4 if version == 2 else 8
     header_size = RAW_HEADER_INTS * 4 + num_chunks * off_size
@@ -200,6 +204,47 @@ def raw_fwd_bytes(values: np.ndarray, stored_type: str, version: int = 4, docs_p
         pos += len(blk)
     hdr += struct.pack(">%d%s" % (num_chunks, "i" if off_size == 4 else "q"), *offs)
     return hdr + b"".join(chunks)
+
+
+def _delta_chunk(raw: bytes, dd: bool) -> bytes:
+    """DeltaCompressor / DeltaDeltaCompressor.compress (io/compression/DeltaCompressor.java:45-150):
+    LONG layout when the chunk is a multiple of 8 bytes (even for INT columns), else INT; flag byte,
+    BE count, BE first value, BE LZ4-block size, LZ4 block of BE deltas (DELTADELTA: first delta, then
+    deltas of deltas), all with Java's wrapping arithmetic."""
+    w = 8 if len(raw) % 8 == 0 else 4
+    v = np.frombuffer(raw, dtype=">u8" if w == 8 else ">u4").astype(np.uint64 if w == 8 else np.uint32)
+    out = struct.pack(">bi", 1 if w == 8 else 0, v.size)
+    if v.size == 0:
+        return out
+    out += raw[:w]
+    if v.size == 1:
+        return out
+    d = np.diff(v)  # unsigned wrap-around == Java's overflowing subtraction
+    if dd:
+        d = np.r_[d[:1], np.diff(d)]
+    blk = lz4_block_compress(d.astype(">u8" if w == 8 else ">u4").tobytes())
+    return out + struct.pack(">i", len(blk)) + blk
+
+
+def chunk_compress(raw: bytes, compression: int) -> bytes:
+    """One chunk through ChunkCompressorFactory's compressor for `compression`
+    (pinot-segment-local/.../io/compression/*Compressor.java). SNAPPY / ZSTANDARD come from pyarrow's
+    bundled codecs (raw snappy block; zstd frame with content size), standing in for snappy-java /
+    zstd-jni on the write side only: the readers under test decode them independently."""
+    if compression in (LZ4, LZ4_LENGTH_PREFIXED):
+        blk = lz4_block_compress(raw)
+        if compression == LZ4_LENGTH_PREFIXED:  # LZ4CompressorWithLength: decompressed length, LE int
+            blk = struct.pack("<i", len(raw)) + blk
+        return blk
+    if compression in (SNAPPY, ZSTANDARD):
+        import pyarrow as pa
+        return pa.Codec("snappy" if compression == SNAPPY else "zstd").compress(raw, asbytes=True)
+    if compression == GZIP:  # java.util.zip.Deflater (zlib stream) + BE uncompressed size
+        import zlib
+        return zlib.compress(raw) + struct.pack(">i", len(raw))
+    if compression in (DELTA, DELTADELTA):
+        return _delta_chunk(raw, compression == DELTADELTA)
+    raise NotImplementedError(f"compression {compression}")
 
 
 def raw_fwd_header(n: int, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:

@@ -173,6 +173,57 @@ def test_lz4_known_block():
     assert bytes(dst[:n]) == b"a" * 21 + b"bcdef"
 
 
+ALL_CODECS = [S.SNAPPY, S.ZSTANDARD, S.LZ4, S.LZ4_LENGTH_PREFIXED, S.GZIP, S.DELTA, S.DELTADELTA]
+
+
+def _codec_values(t, n, rng):
+    if t in (S.INT, S.LONG):
+        info = np.iinfo(np.int32 if t == S.INT else np.int64)
+        v = np.cumsum(rng.integers(-3, 9, n)).astype(np.int64) + 1_600_000_000  # timestamp-like runs
+        v[::97] = info.max  # wrap-around deltas
+        v[1::131] = info.min
+        return v.astype(np.int32 if t == S.INT else np.int64)
+    return (rng.integers(0, 40, n) * 0.5).astype(np.float32 if t == S.FLOAT else np.float64)
+
+
+@pytest.mark.parametrize("comp", ALL_CODECS)
+@pytest.mark.parametrize("t", [S.INT, S.LONG, S.FLOAT, S.DOUBLE])
+def test_chunk_codecs_roundtrip_through_oracle(comp, t):
+    """Every ChunkCompressionType (ChunkCompressionType.java:22) written chunk by chunk and read back
+    by the oracle's decompressors. 7001 INT values in 1024-doc chunks exercise both of DELTA's
+    layouts: full chunks are a multiple of 8 bytes (LONG flag), the ragged last chunk is not."""
+    if comp in (S.DELTA, S.DELTADELTA) and t not in (S.INT, S.LONG):
+        pytest.skip("DELTA codecs hold INT/LONG values")
+    v = _codec_values(t, 7001, np.random.default_rng(comp * 10 + len(t)))
+    col = S.build_column("c", v, t, dictionary=False, compression=comp)
+    h = S.parse_raw_fwd_header(col.fwd)
+    assert h.compression == comp and h.num_chunks == 7
+    raw = oracle.raw_values_region(col)
+    got = np.frombuffer(raw[:v.nbytes].tobytes(), dtype=v.dtype.newbyteorder(">"))
+    assert np.array_equal(got, v)
+
+
+def test_snappy_known_block():
+    # varint length 9, literal "abc", copy-1 (length 6, offset 3, overlapping) -> "abcabcabc"
+    blk = bytes([9, 0x08]) + b"abc" + bytes([0x09, 0x03])
+    dst = (C.c_uint8 * 16)()
+    assert oracle.lib().oracle_snappy_decompress(blk, len(blk), dst, 16) == 9
+    assert bytes(dst[:9]) == b"abcabcabc"
+    assert oracle.lib().oracle_snappy_decompress(blk[:-1], len(blk) - 1, dst, 16) == -1  # truncated
+
+
+def test_delta_known_chunk():
+    # DeltaCompressor INT layout for [5, 7, 4]: flag 0, count 3, first 5, LZ4(deltas 2, -3)
+    d = S.lz4_block_compress(np.array([2, -3], dtype=">i4").tobytes())
+    blk = bytes([0]) + (3).to_bytes(4, "big") + (5).to_bytes(4, "big") + len(d).to_bytes(4, "big") + d
+    dst = (C.c_uint8 * 12)()
+    assert oracle.lib().oracle_delta_decompress(blk, len(blk), dst, 12, 0) == 12
+    assert np.array_equal(np.frombuffer(bytes(dst), dtype=">i4"), [5, 7, 4])
+    # the same bytes as DELTADELTA: first delta 2, then delta-of-delta -3 -> [5, 7, 6]
+    assert oracle.lib().oracle_delta_decompress(blk, len(blk), dst, 12, 1) == 12
+    assert np.array_equal(np.frombuffer(bytes(dst), dtype=">i4"), [5, 7, 6])
+
+
 def test_vectorised_inverted_index_matches_general_builder():
     """inverted_index_bytes_fast (numpy) == one roaring_serialize per bitmap, byte for byte, and
     declines inputs that need bitmap or run containers."""
