@@ -401,7 +401,7 @@ def test_nan_min_max_semantics(engine, t, kernel_mode):
     """NaN in a raw FLOAT/DOUBLE column: aggregation-only MIN/MAX fold with Math.min/Math.max and
     return NaN (MinAggregationFunction.java:115-119); GROUP BY MIN/MAX compare with `value < min`
     and skip it (MinAggregationFunction.java:247-250). Groups without NaN must be unaffected."""
-    rng = np.random.default_rng(11 + t)
+    rng = np.random.default_rng(11 + len(t))
     n = 30_011
     npt = np.float32 if t == S.FLOAT else np.float64
     v = (rng.integers(-5000, 5000, n) * 0.25).astype(npt)
