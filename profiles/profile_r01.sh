@@ -19,4 +19,4 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out
 echo pmc3 done
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv -d gpurun_out/prof/pmc2 -o run -- python3 bench.py --steps 3 --warmup 1 --segments 40 --no-cpu-baseline > /dev/null 2> gpurun_out/prof/pmc2.err
 echo pmc2 done
-python3 profiles/summarize.py gpurun_out/prof profiles/r01
+python3 profiles/summarize.py gpurun_out/prof gpurun_out/prof_summary
