@@ -175,7 +175,11 @@ int pinot_amd_query_destroy(pinot_amd_query* q);
  * or negate=1). */
 int pinot_amd_query_add_predicate(pinot_amd_query* q, int32_t clause, const pinot_amd_predicate_spec* p,
                                   int32_t negate);
-/* GROUP BY on dictionary-encoded columns (DictionaryBasedGroupKeyGenerator). */
+/* GROUP BY on dictionary-encoded columns (DictionaryBasedGroupKeyGenerator.java:116-180) or on raw
+ * INT/LONG/FLOAT/DOUBLE columns (NoDictionarySingleColumnGroupKeyGenerator.java:98-143,
+ * NoDictionaryMultiColumnGroupKeyGenerator: one group per distinct value, FLOAT/DOUBLE told apart by
+ * floatToIntBits/doubleToLongBits). A raw column gets a derived dictionary twin staged on its segment
+ * at the first such query (kept for later queries). */
 int pinot_amd_query_add_group_by(pinot_amd_query* q, const char* column);
 /* Aggregation function (column NULL or "*" for COUNT(*)). Returns the aggregation index via out_index. */
 int pinot_amd_query_add_aggregation(pinot_amd_query* q, int32_t agg_type, const char* column, int32_t* out_index);

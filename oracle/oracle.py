@@ -221,7 +221,8 @@ class OracleSegment:
         self.names = list(seg.columns)
         self.index = {n: i for i, n in enumerate(self.names)}
         self._keep = []
-        cols = (OColumn * len(self.names))()
+        cols = (OColumn * (2 * len(self.names)))()  # second half: raw columns' group ids, on demand
+        self._raw_groups = {}
         for i, n in enumerate(self.names):
             cb = seg.columns[n]
             oc = cols[i]
@@ -310,11 +311,42 @@ class OracleSegment:
         cnt = lib().oracle_filter(self.cols, n, leaves, nl, _ptr(bits))
         return bits, int(cnt)
 
+    def group_col(self, g: str) -> int:
+        """Column index that yields group ids for GROUP BY g. Dictionary columns group by dictId
+        (DictionaryBasedGroupKeyGenerator); raw columns by value (NoDictionarySingleColumnGroupKeyGenerator
+        .java:98-143: a fastutil open hash map per stored type, whose key equality for FLOAT/DOUBLE is
+        floatToIntBits/doubleToLongBits, i.e. all NaNs equal and -0.0 != 0.0). Restated as ids into the
+        distinct canonical bit patterns of the column."""
+        cb = self.seg.columns[g]
+        if cb.encoding != "RAW":
+            return self.index[g]
+        if g not in self._raw_groups:
+            vals = np.frombuffer(raw_values_region(cb).tobytes(), dtype=np.dtype(
+                {INT: ">i4", LONG: ">i8", FLOAT: ">f4", DOUBLE: ">f8"}[cb.stored_type]),
+                count=self.seg.num_docs).astype(np.dtype({INT: "i4", LONG: "i8", FLOAT: "f4", DOUBLE: "f8"}[cb.stored_type]))
+            if cb.stored_type in (FLOAT, DOUBLE):
+                bits = vals.view(np.uint32 if cb.stored_type == FLOAT else np.uint64).copy()
+                bits[np.isnan(vals)] = 0x7FC00000 if cb.stored_type == FLOAT else 0x7FF8000000000000
+                uniq, ids = np.unique(bits, return_inverse=True)
+                dvals = uniq.view(vals.dtype)
+            else:
+                dvals, ids = np.unique(vals, return_inverse=True)
+            ids = np.ascontiguousarray(ids.astype(np.int32))
+            i = len(self.names) + self.index[g]
+            oc = self.cols[i]
+            oc.encoding = 3  # OR_ENC_IDS
+            oc.stored_type = OR_TYPE[cb.stored_type]
+            oc.cardinality = len(dvals)
+            oc.fwd = _ptr(ids)
+            self._keep.append(ids)
+            self._raw_groups[g] = (i, dvals)
+        return self._raw_groups[g][0]
+
     def key_values(self, dict_ids, group_by: Sequence[str]) -> tuple:
         out = []
         for g, d in zip(group_by, dict_ids):
             cb = self.seg.columns[g]
-            v = cb.dict_values[int(d)]
+            v = self._raw_groups[g][1][int(d)] if g in self._raw_groups else cb.dict_values[int(d)]
             out.append(v if cb.stored_type == STRING else (float(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
         return tuple(out)
 
@@ -359,7 +391,7 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
             keys = np.zeros(cap * len(qc.group_by), dtype=np.int32)
             vals = np.zeros(cap * len(nat), dtype=np.float64)
             vali = np.zeros(cap * len(nat), dtype=np.int64)
-            gcols = np.array([os_.index[g] for g in qc.group_by], dtype=np.int32)
+            gcols = np.array([os_.group_col(g) for g in qc.group_by], dtype=np.int32)
             ng = lib().oracle_group_by(os_.cols, seg.num_docs, bptr, _ptr(gcols), len(gcols), aggs, len(nat), cap,
                                        _ptr(keys), _ptr(vals), _ptr(vali))
             assert ng >= 0, ng

@@ -124,6 +124,7 @@ double oracle_raw_read_f64(const uint8_t* raw, int32_t type, int64_t index) {
 }
 
 static int32_t dict_id_of(const oracle_column* c, int64_t doc) {
+  if (c->encoding == OR_ENC_IDS) return ((const int32_t*)c->fwd)[doc];
   if (c->encoding == OR_ENC_SORTED) return oracle_sorted_dict_id(c->fwd, c->cardinality, doc);
   return oracle_fixedbit_read(c->fwd, c->bits, doc);
 }

@@ -22,7 +22,9 @@ extern "C" {
 /* stored types (FieldSpec.DataType stored types on the path) */
 enum { OR_INT = 0, OR_LONG = 1, OR_FLOAT = 2, OR_DOUBLE = 3 };
 /* forward-index encodings */
-enum { OR_ENC_FIXED_BIT = 0, OR_ENC_RAW = 1, OR_ENC_SORTED = 2 };
+/* OR_ENC_IDS: a plain int32 group id per doc, the value -> id map a raw column's group key generator
+ * builds (NoDictionarySingleColumnGroupKeyGenerator.java:98-143); fwd = int32[num_docs] */
+enum { OR_ENC_FIXED_BIT = 0, OR_ENC_RAW = 1, OR_ENC_SORTED = 2, OR_ENC_IDS = 3 };
 /* predicate leaf kinds */
 enum {
   OR_PRED_DICT_RANGE = 0,   /* dictId in [lo, hi)            SortedDictionaryBasedRangePredicateEvaluator */

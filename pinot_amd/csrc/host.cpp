@@ -1050,6 +1050,94 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
   return 0;
 }
 
+// Double.compare / Double.doubleToLongBits order: -0.0 < 0.0, every NaN equal and greatest. Group
+// keys of FLOAT/DOUBLE columns are told apart this way (fastutil's Double2IntOpenHashMap compares
+// doubleToLongBits; sorted dictionaries use Double.compare), so merged key columns sort by it.
+static uint64_t java_double_order(double v) {
+  uint64_t b;
+  if (std::isnan(v)) b = 0x7ff8000000000000ull;
+  else memcpy(&b, &v, 8);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+static double java_double_from_order(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  double v;
+  memcpy(&v, &b, 8);
+  return v;
+}
+static bool java_double_less(double a, double b) { return java_double_order(a) < java_double_order(b); }
+
+// GROUP BY on a raw (no-dictionary) column: NoDictionarySingleColumnGroupKeyGenerator /
+// NoDictionaryMultiColumnGroupKeyGenerator (pinot-core/.../query/aggregation/groupby/
+// NoDictionarySingleColumnGroupKeyGenerator.java:98-143) assign group ids to distinct values through
+// fastutil open hash maps (equality = value equality, doubleToLongBits for FLOAT/DOUBLE). Here the
+// segment gets a derived dictionary-encoded twin of the column, built once on first use and kept
+// staged next to it ("<col>$dict": sorted distinct values in the same order as a Pinot dictionary +
+// a fixed-bit forward index of dictIds), so the device plan groups it exactly like a dictionary
+// column: same groups, same key values, same dense mixed-radix key space.
+static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& col, std::string* out_name) {
+  *out_name = col + "$dict";
+  if (s->cols.count(*out_name)) return 0;
+  const Column& c = *s->cols.at(col);
+  if (c.type == T_STRING) return fail(PINOT_AMD_EUNSUPPORTED, "GROUP BY on raw STRING column %s", col.c_str());
+  const int64_t nd = s->num_docs;
+  const int vs = value_size(c.type);
+  std::vector<uint8_t> be((size_t)nd * vs);
+  if (nd) HIP_OK(hipMemcpy(be.data(), c.fwd.p, be.size(), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> key((size_t)nd);  // order-preserving key per doc
+  for (int64_t d = 0; d < nd; ++d) {
+    const uint8_t* p = be.data() + (size_t)d * vs;
+    uint64_t u = 0;
+    for (int i = 0; i < vs; ++i) u = (u << 8) | p[i];
+    switch (c.type) {
+      case T_INT: key[d] = (uint64_t)(int64_t)(int32_t)(uint32_t)u ^ (1ull << 63); break;
+      case T_LONG: key[d] = u ^ (1ull << 63); break;
+      case T_FLOAT: { uint32_t b = (uint32_t)u; float f; memcpy(&f, &b, 4); key[d] = java_double_order((double)f); break; }
+      default: { double f; memcpy(&f, &u, 8); key[d] = java_double_order(f); break; }
+    }
+  }
+  std::vector<uint64_t> uniq(key);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  const int32_t card = (int32_t)uniq.size();
+  int bits = 1;
+  while (card > 1 && (1ll << bits) < (int64_t)card) ++bits;  // PinotDataBitSet.getNumBitsPerValue(card - 1)
+  // fixed-bit stream, MSB first (FixedBitSVForwardIndexWriter)
+  std::vector<uint8_t> fb((size_t)((nd * bits + 7) / 8) + 8, 0);
+  uint64_t acc = 0;
+  int nacc = 0;
+  size_t o = 0;
+  for (int64_t d = 0; d < nd; ++d) {
+    const uint64_t id = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), key[d]) - uniq.begin());
+    acc = (acc << bits) | id;
+    nacc += bits;
+    while (nacc >= 8) { fb[o++] = (uint8_t)(acc >> (nacc - 8)); nacc -= 8; }
+  }
+  if (nacc > 0) fb[o++] = (uint8_t)(acc << (8 - nacc));
+  // dictionary: big-endian fixed-width values in sorted order
+  std::vector<uint8_t> dict((size_t)card * vs);
+  for (int32_t i = 0; i < card; ++i) {
+    uint64_t u;
+    switch (c.type) {
+      case T_INT: case T_LONG: u = uniq[i] ^ (1ull << 63); break;
+      case T_FLOAT: { float f = (float)java_double_from_order(uniq[i]); uint32_t b; memcpy(&b, &f, 4); u = b; break; }
+      default: { double f = java_double_from_order(uniq[i]); memcpy(&u, &f, 8); break; }
+    }
+    for (int b = 0; b < vs; ++b) dict[(size_t)i * vs + b] = (uint8_t)(u >> (8 * (vs - 1 - b)));
+  }
+  pinot_amd_column_spec spec{};
+  spec.name = out_name->c_str();
+  spec.stored_type = c.type;
+  spec.encoding = ENC_FIXED_BIT;
+  spec.cardinality = card;
+  spec.bits_per_element = bits;
+  spec.h_fwd = fb.data();
+  spec.fwd_size = fb.size();
+  spec.h_dictionary = dict.data();
+  spec.dictionary_size = dict.size();
+  return pinot_amd_segment_add_column(s, &spec);
+}
+
 static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
                              MergedKeyColumn* out) {
   const Column* c0 = segs[0]->cols.at(col).get();
@@ -1065,8 +1153,10 @@ static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const 
     std::sort(out->vs.begin(), out->vs.end(), java_less);
     out->vs.erase(std::unique(out->vs.begin(), out->vs.end()), out->vs.end());
   } else if (is_float(out->type)) {
-    std::sort(out->vd.begin(), out->vd.end());
-    out->vd.erase(std::unique(out->vd.begin(), out->vd.end()), out->vd.end());
+    std::sort(out->vd.begin(), out->vd.end(), java_double_less);
+    out->vd.erase(std::unique(out->vd.begin(), out->vd.end(),
+                              [](double a, double b) { return java_double_order(a) == java_double_order(b); }),
+                  out->vd.end());
   } else {
     std::sort(out->vi.begin(), out->vi.end());
     out->vi.erase(std::unique(out->vi.begin(), out->vi.end()), out->vi.end());
@@ -1081,7 +1171,7 @@ static int remap_for(const Column& c, const MergedKeyColumn& m, std::vector<int3
     if (c.type == T_STRING)
       pos = std::lower_bound(m.vs.begin(), m.vs.end(), c.dict_s[d], java_less) - m.vs.begin();
     else if (is_float(c.type))
-      pos = std::lower_bound(m.vd.begin(), m.vd.end(), c.dict_d[d]) - m.vd.begin();
+      pos = std::lower_bound(m.vd.begin(), m.vd.end(), c.dict_d[d], java_double_less) - m.vd.begin();
     else
       pos = std::lower_bound(m.vi.begin(), m.vi.end(), c.dict_i[d]) - m.vi.begin();
     (*out)[d] = (int32_t)pos;
@@ -1147,7 +1237,23 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   r->stream = (hipStream_t)stream;
   pinot_amd_query filter_q;
   if (filter_only) filter_q.preds = qq->preds;  // FilterPlanNode only: no projection, no aggregation
-  const pinot_amd_query& Q = filter_only ? filter_q : *qq;
+  const pinot_amd_query* Qp = filter_only ? &filter_q : qq;
+  pinot_amd_query raw_gb_q;  // group-by columns redirected to the derived dictionary of raw columns
+  for (size_t j = 0; j < Qp->group_by.size(); ++j) {
+    const std::string& g = Qp->group_by[j];
+    int nraw = 0;
+    for (auto* s : segs) {
+      auto it = s->cols.find(g);
+      if (it == s->cols.end()) return fail(PINOT_AMD_EINVAL, "segment %s has no column %s", s->name.c_str(), g.c_str());
+      nraw += it->second->enc == ENC_RAW;
+    }
+    if (nraw == 0) continue;
+    if (nraw != n) return fail(PINOT_AMD_EUNSUPPORTED, "GROUP BY column %s is raw in some segments only", g.c_str());
+    if (Qp != &raw_gb_q) { raw_gb_q = *Qp; Qp = &raw_gb_q; }
+    for (auto* s : segs)
+      if (int rc = derive_raw_group_dictionary(s, g, &raw_gb_q.group_by[j])) return rc;
+  }
+  const pinot_amd_query& Q = *Qp;
 
   // ---- slots: columns the kernel must decode ----
   std::vector<std::string> slot_cols;
@@ -1172,8 +1278,6 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   // group-by + aggregation columns always need decoding; predicate columns only if some segment's
   // leaf reads values (decided below)
   for (auto& g : Q.group_by) {
-    const Column& c = *segs[0]->cols.at(g);
-    if (c.enc == ENC_RAW) return fail(PINOT_AMD_EUNSUPPORTED, "GROUP BY on raw column %s", g.c_str());
     slot_of(g);
   }
   for (auto& a : Q.aggs) {

@@ -494,3 +494,54 @@ def test_malformed_chunk_fails_loudly(engine, comp):
 def dataclasses_replace(obj, **kw):
     import dataclasses
     return dataclasses.replace(obj, **kw)
+
+
+@pytest.mark.parametrize("t", [S.INT, S.LONG, S.FLOAT, S.DOUBLE])
+def test_group_by_raw_column(engine, t, kernel_mode):
+    """GROUP BY on raw columns (NoDictionarySingleColumnGroupKeyGenerator.java:98-143,
+    NoDictionaryMultiColumnGroupKeyGenerator): one group per distinct value. The device groups through
+    a derived dictionary twin built at first use; three segments with overlapping, different value
+    sets exercise the merged key space; the raw column is also filtered on and aggregated (same
+    column, raw slot) and combined with a dictionary column in a multi-column key."""
+    rng = np.random.default_rng(40 + len(t))
+    npt = {S.INT: np.int32, S.LONG: np.int64, S.FLOAT: np.float32, S.DOUBLE: np.float64}[t]
+    segs, bufs_l = [], []
+    for si, n in enumerate([30_011, 17_003, 45_000]):
+        base = rng.integers(-200 + 50 * si, 200 + 50 * si, n)
+        k = (base * (1 << 34) + 7).astype(npt) if t == S.LONG else (base * 0.25).astype(npt) if t in (S.FLOAT, S.DOUBLE) \
+            else (base * 1000).astype(npt)
+        comp = [S.PASS_THROUGH, S.LZ4, S.SNAPPY][si]
+        b = S.build_segment(f"rawgb{si}", {
+            "k": (k, t, {"dictionary": False, "compression": comp}),
+            "d": (rng.integers(0, 9, n).astype(np.int32), S.INT, {}),
+            "v": (rng.integers(-1000, 1000, n).astype(np.int32), S.INT, {"dictionary": False})})
+        bufs_l.append(b)
+        segs.append(engine.ImmutableSegment(b))
+    ex = engine.ServerQueryExecutor()
+    for q in ["SELECT k, COUNT(*), SUM(v), MIN(v), MAX(v) FROM t GROUP BY k",
+              "SELECT k, d, COUNT(*), SUM(v), MAX(k) FROM t WHERE k > 0 AND v < 700 GROUP BY k, d",
+              "SELECT d, k, SUM(k), MIN(k) FROM t WHERE d IN (1, 3, 5) GROUP BY d, k"]:
+        res = ex.execute(q, segs)
+        check_mode(res, kernel_mode)
+        nm, og = oracle.execute(q, bufs_l)
+        assert res.num_docs_matched() == nm, q
+        assert_same_groups(res.groups(), og)
+
+
+def test_group_by_raw_high_cardinality(engine, kernel_mode):
+    """A raw LONG key with ~150k distinct values (a key space past the LDS tables: direct-atomic or
+    partitioned plan) matches the oracle's value grouping; re-execution reuses the derived dictionary."""
+    rng = np.random.default_rng(77)
+    n = 400_000
+    k = rng.integers(0, 150_000, n).astype(np.int64) * 3 - 10**12
+    v = rng.integers(0, 1 << 20, n).astype(np.int64)
+    b = S.build_segment("rawhc", {"k": (k, S.LONG, {"dictionary": False}),
+                                  "v": (v, S.LONG, {"dictionary": False})})
+    seg = engine.ImmutableSegment(b)
+    q = "SET numGroupsLimit = 1000000; SELECT k, COUNT(*), SUM(v), MIN(v), MAX(v) FROM t WHERE v > 1000 GROUP BY k"
+    ex = engine.ServerQueryExecutor()
+    _, og = oracle.execute(q, [b])
+    for _ in range(2):
+        res = ex.execute(q, [seg])
+        check_mode(res, kernel_mode)
+        assert_same_groups(res.groups(), og)
