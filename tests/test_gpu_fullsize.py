@@ -1,0 +1,93 @@
+"""Parity at BASELINE.json's full size (configs[1]: 1B rows in 100 segments of 10M rows, the bench
+table and query) through size-independent properties, since the oracle cannot run 1B rows in a test:
+
+* combine linearity: the result over all 100 segments equals the AggregationFunction.merge of the
+  results over two disjoint segment subsets (GroupByCombineOperator's merge; exact for COUNT, integer
+  SUM and MAX, 1e-12 relative for double SUM);
+* per-segment spot checks: the first and last segment through the HIP path equal the CPU oracle;
+* counting identities: COUNT(*) without a filter is 1e9; the COUNTs of a range, of everything below it
+  and of everything above it add up to 1e9; the group COUNTs add up to numDocsMatched.
+"""
+import math
+
+import pytest
+
+import oracle
+from pinot_amd import datagen
+from pinot_amd.query import merge_partial
+
+pytestmark = pytest.mark.gpu
+
+NSEG, ROWS = 100, 10_000_000
+RTOL = 1e-12  # double SUM: order-dependent in both implementations (north_star tolerance)
+
+
+@pytest.fixture(scope="module")
+def table():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    from pinot_amd import engine as E
+    segs, spot = [], {}
+    for i in range(NSEG):
+        b = datagen.ad_segment(f"full{i}", ROWS, seed=i)
+        segs.append(E.ImmutableSegment(b))
+        if i in (0, NSEG - 1):
+            spot[i] = b
+        del b
+    return E, segs, spot
+
+
+def _close(a, b):
+    if isinstance(a, float):
+        return math.isclose(a, b, rel_tol=RTOL, abs_tol=0.0)
+    return a == b
+
+
+@pytest.mark.timeout(900)
+def test_full_size_combine_linearity(table):
+    E, segs, _ = table
+    ex = E.ServerQueryExecutor()
+    q = datagen.BENCH_QUERY
+    full = ex.execute(q, segs)
+    assert full.kernel_info().startswith("jit")
+    g_full = full.groups()
+    a = ex.execute(q, segs[:37]).groups()
+    b = ex.execute(q, segs[37:]).groups()
+    funcs = ["COUNT", "SUM", "SUM", "SUM", "MAX"]
+    merged = dict(a)
+    for k, v in b.items():
+        merged[k] = [merge_partial(f, x, y) for f, x, y in zip(funcs, merged[k], v)] if k in merged else v
+    assert set(merged) == set(g_full) and len(g_full) == 201
+    for k, v in g_full.items():
+        for i, (x, y) in enumerate(zip(v, merged[k])):
+            assert _close(x, y), (k, i, x, y)
+    assert sum(v[0] for v in g_full.values()) == full.num_docs_matched()
+
+
+@pytest.mark.timeout(900)
+def test_full_size_counting_identities(table):
+    E, segs, _ = table
+    ex = E.ServerQueryExecutor()
+    lo, hi = datagen.DAYS_BASE + 100, datagen.DAYS_BASE + 300
+    (total,) = ex.execute("SELECT COUNT(*) FROM t", segs).groups()[()]
+    assert total == NSEG * ROWS
+    parts = [ex.execute(f"SELECT COUNT(*) FROM t WHERE {w}", segs).groups()[()][0]
+             for w in (f"daysSinceEpoch BETWEEN {lo} AND {hi}", f"daysSinceEpoch < {lo}", f"daysSinceEpoch > {hi}")]
+    assert sum(parts) == total
+    clicks = [ex.execute(f"SELECT COUNT(*) FROM t WHERE {w}", segs).groups()[()][0]
+              for w in ("clicks > 100", "clicks <= 100")]
+    assert sum(clicks) == total
+
+
+@pytest.mark.timeout(900)
+def test_full_size_spot_segments_vs_oracle(table):
+    E, segs, spot = table
+    ex = E.ServerQueryExecutor()
+    q = datagen.BENCH_QUERY
+    for i, bufs in spot.items():
+        got = ex.execute(q, [segs[i]]).groups()
+        _, exp = oracle.execute(q, [bufs])
+        assert set(got) == set(exp)
+        for k, e in exp.items():
+            for j, (x, y) in enumerate(zip(got[k], e)):
+                assert _close(x, y), (i, k, j, x, y)
