@@ -91,3 +91,45 @@ def test_full_size_spot_segments_vs_oracle(table):
         for k, e in exp.items():
             for j, (x, y) in enumerate(zip(got[k], e)):
                 assert _close(x, y), (i, k, j, x, y)
+
+
+# ------------------------------------------------------------------ configs[3] at full per-GPU size
+@pytest.mark.timeout(900)
+def test_full_size_highcard_partitioned_vs_atomic_and_linearity(monkeypatch):
+    """configs[3] per GPU: 1B rows in 100 segments, ~1M (dimA, dimB) groups. The partitioned plan
+    (count / scatter / LDS-aggregate) must equal the direct HBM-atomic plan group by group (COUNT,
+    integer SUM, MIN(LONG), MAX(DOUBLE) are all order-independent, so exactly), the result must be the
+    merge of two disjoint segment subsets, and the first segment must equal the oracle."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import engine as E
+    segs, spot = [], None
+    for i in range(NSEG):
+        b = datagen.highcard_segment(f"hc{i}", ROWS, seed=1000 + i)
+        segs.append(E.ImmutableSegment(b))
+        if i == 0:
+            spot = b
+        del b
+    q = datagen.HIGHCARD_QUERY
+    ex = E.ServerQueryExecutor()
+    monkeypatch.setenv("PINOT_AMD_PARTITIONED", "1")
+    part = ex.execute(q, segs)
+    assert "partitioned" in part.kernel_info(), part.kernel_info()
+    assert not part.num_groups_limit_reached()
+    g_part = part.groups()
+    assert len(g_part) > 900_000
+    assert sum(v[0] for v in g_part.values()) == part.num_docs_matched()
+    a = ex.execute(q, segs[:50]).groups()
+    b = ex.execute(q, segs[50:]).groups()
+    funcs = ["COUNT", "SUM", "MIN", "MAX"]
+    for k, v in b.items():
+        a[k] = [merge_partial(f, x, y) for f, x, y in zip(funcs, a[k], v)] if k in a else v
+    assert a == g_part
+    del a, b
+    monkeypatch.setenv("PINOT_AMD_PARTITIONED", "0")
+    atomic = ex.execute(q, segs)
+    assert "partitioned" not in atomic.kernel_info()
+    assert atomic.groups() == g_part
+    got = ex.execute(q, [segs[0]]).groups()
+    _, exp = oracle.execute(q, [spot])
+    assert got == exp
