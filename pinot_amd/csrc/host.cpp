@@ -14,6 +14,9 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <new>
+#include <stdexcept>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1085,7 +1088,14 @@ static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& 
   std::vector<uint8_t> be((size_t)nd * vs);
   if (nd) HIP_OK(hipMemcpy(be.data(), c.fwd.p, be.size(), hipMemcpyDeviceToHost));
   std::vector<uint64_t> key((size_t)nd);  // order-preserving key per doc
-  for (int64_t d = 0; d < nd; ++d) {
+  auto parallel = [nd](auto&& body) {  // [d0, d1) ranges over host threads
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, nd / (1 << 16)));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { body(nd * t / nt, nd * (t + 1) / nt); });
+    for (auto& x : th) x.join();
+  };
+  parallel([&](int64_t d0, int64_t d1) {
+  for (int64_t d = d0; d < d1; ++d) {
     const uint8_t* p = be.data() + (size_t)d * vs;
     uint64_t u = 0;
     for (int i = 0; i < vs; ++i) u = (u << 8) | p[i];
@@ -1096,6 +1106,7 @@ static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& 
       default: { double f; memcpy(&f, &u, 8); key[d] = java_double_order(f); break; }
     }
   }
+  });
   std::vector<uint64_t> uniq(key);
   std::sort(uniq.begin(), uniq.end());
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
@@ -1107,8 +1118,12 @@ static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& 
   uint64_t acc = 0;
   int nacc = 0;
   size_t o = 0;
+  parallel([&](int64_t d0, int64_t d1) {  // key -> dictId, in place
+    for (int64_t d = d0; d < d1; ++d)
+      key[d] = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), key[d]) - uniq.begin());
+  });
   for (int64_t d = 0; d < nd; ++d) {
-    const uint64_t id = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), key[d]) - uniq.begin());
+    const uint64_t id = key[d];
     acc = (acc << bits) | id;
     nacc += bits;
     while (nacc >= 8) { fb[o++] = (uint8_t)(acc >> (nacc - 8)); nacc -= 8; }
@@ -1359,7 +1374,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (rc) return rc;
     r->key_stride.push_back(num_keys);
     const double nk = (double)num_keys * (double)std::max<size_t>(m.size(), 1);
-    if (nk > (double)(1ll << 31)) return fail(PINOT_AMD_EUNSUPPORTED, "group key space %.0f exceeds the dense table", nk);
+    // dense tables stop at 2^28 keys (2 GiB per accumulator array); sparser spaces stay on the Java path
+    if (nk > (double)(1ll << 28)) return fail(PINOT_AMD_EUNSUPPORTED, "group key space %.0f exceeds the dense table", nk);
     num_keys *= (int64_t)std::max<size_t>(m.size(), 1);
     r->keys.push_back(std::move(m));
   }
@@ -1755,14 +1771,29 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   return 0;
 }
 
+// No C++ exception may cross the C ABI: a host allocation failure (a huge dense key space, a derived
+// dictionary of a huge segment) comes back as PINOT_AMD_ENOMEM like a failed hipMalloc.
+extern "C++" {
+template <class F>
+static int no_throw(const char* what, F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(PINOT_AMD_ENOMEM, "%s: host allocation failed", what);
+  } catch (const std::exception& e) {
+    return fail(PINOT_AMD_EINVAL, "%s: %s", what, e.what());
+  }
+}
+}
+
 int pinot_amd_execute(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
                       pinot_amd_result** out) {
-  return execute_impl(qq, segs_in, n, stream, false, out);
+  return no_throw("execute", [&] { return execute_impl(qq, segs_in, n, stream, false, out); });
 }
 
 int pinot_amd_execute_filter(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
                              pinot_amd_result** out) {
-  return execute_impl(qq, segs_in, n, stream, true, out);
+  return no_throw("execute_filter", [&] { return execute_impl(qq, segs_in, n, stream, true, out); });
 }
 
 int pinot_amd_result_bitset(pinot_amd_result* r, int32_t segment_index, const uint64_t** h_d_bitset,
@@ -1817,7 +1848,11 @@ int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms) {
 
 static int fetch_acc(pinot_amd_result* r, std::vector<uint64_t>* h) {
   const int64_t nk = r->q.num_keys;
-  h->resize((size_t)std::max(r->q.nacc, 1) * nk);
+  try {
+    h->resize((size_t)std::max(r->q.nacc, 1) * nk);
+  } catch (const std::bad_alloc&) {
+    return fail(PINOT_AMD_ENOMEM, "fetch: %lld accumulator slots do not fit host memory", (long long)(r->q.nacc * nk));
+  }
   if (r->q.nacc == 0) return 0;
   HIP_OK(hipMemcpyAsync(h->data(), r->acc.p, h->size() * 8, hipMemcpyDeviceToHost, r->stream));
   HIP_OK(hipStreamSynchronize(r->stream));

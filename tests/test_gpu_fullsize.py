@@ -133,3 +133,41 @@ def test_full_size_highcard_partitioned_vs_atomic_and_linearity(monkeypatch):
     got = ex.execute(q, [segs[0]]).groups()
     _, exp = oracle.execute(q, [spot])
     assert got == exp
+
+
+# ------------------------------------------------------------------ configs[4] at full size (SF100)
+@pytest.mark.timeout(900)
+def test_full_size_ssb_sf100_linearity_and_oracle_segment():
+    """configs[4]: SSB SF100 denormalized lineorder, 600M rows in 60 segments (bench's generator). For
+    each of the 13 queries, the 60-segment result equals the merge of two disjoint subsets (keys
+    exactly, SUMs within 1e-12 relative: they are double sums of CASTs/products), and segment 0
+    equals the CPU oracle."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import engine as E
+    from pinot_amd import ssb
+    from pinot_amd.query import parse_sql
+    segs, spot = [], None
+    for i in range(60):
+        b = ssb.lineorder_flat_segment(f"lo{i}", ROWS, seed=2000 + i)
+        segs.append(E.ImmutableSegment(b))
+        if i == 0:
+            spot = b
+        del b
+    ex = E.ServerQueryExecutor()
+
+    def same(g, e, what):
+        assert set(g) == set(e), what
+        for k in e:
+            for x, y in zip(g[k], e[k]):
+                assert _close(x, y), (what, k, x, y)
+
+    for name, q in ssb.SSB_QUERIES:
+        funcs = [a.func for a in parse_sql(q).aggregations]
+        full = ex.execute(q, segs).groups()
+        a = ex.execute(q, segs[:23]).groups()
+        for k, v in ex.execute(q, segs[23:]).groups().items():
+            a[k] = [merge_partial(f, x, y) for f, x, y in zip(funcs, a[k], v)] if k in a else v
+        same(full, a, name)
+        _, exp = oracle.execute(q, [spot])
+        same(ex.execute(q, [segs[0]]).groups(), exp, name + " segment 0")

@@ -283,7 +283,12 @@ def test_errors_are_loud(engine):
     with pytest.raises(PinotAmdError):
         engine.ServerQueryExecutor().execute("SELECT COUNT(*) FROM t WHERE nope = 1", [seg])
     with pytest.raises(PinotAmdError):
-        engine.ServerQueryExecutor().execute("SELECT r_int, COUNT(*) FROM t GROUP BY r_int", [seg])
+        engine.ServerQueryExecutor().execute("SELECT nope, COUNT(*) FROM t GROUP BY nope", [seg])
+    with pytest.raises(PinotAmdError):
+        # three raw keys of ~1000 distinct values each x a 143-value dictionary key: a key space past
+        # the dense table (2^28 keys)
+        engine.ServerQueryExecutor().execute("SELECT r_int, r_long, r_double, d1, COUNT(*) FROM t "
+                                             "GROUP BY r_int, r_long, r_double, d1", [seg])
 
 
 FILTERS = [
