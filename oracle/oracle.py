@@ -373,6 +373,10 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
                 nat.append(("SUM", a.column, a.expr))
                 nat.append(("COUNT", "*", None))
                 slots.append(("avg", len(nat) - 2, len(nat) - 1))
+            elif a.func == "MINMAXRANGE":  # MinMaxRangeAggregationFunction: MinMaxRangePair(min, max)
+                nat.append(("MIN", a.column, a.expr))
+                nat.append(("MAX", a.column, a.expr))
+                slots.append(("range", len(nat) - 2, len(nat) - 1))
             else:
                 nat.append((a.func, a.column, a.expr))
                 slots.append(("direct", len(nat) - 1))
@@ -418,6 +422,8 @@ def _parts(qc, slots, nat, vals, vali):
     for a, s in zip(qc.aggregations, slots):
         if s[0] == "avg":
             out.append((float(vals[s[1]]), int(vali[s[2]])))
+        elif s[0] == "range":
+            out.append((float(vals[s[1]]), float(vals[s[2]])))
         elif a.func in ("COUNT", "SUMLONG"):
             out.append(int(vali[s[1]]))
         else:

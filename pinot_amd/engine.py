@@ -231,6 +231,8 @@ class QueryResult:
                     s = vals[g * nnat + slot[1]]
                     c = vals_i[g * nnat + slot[2]]
                     parts.append((float(s), int(c)))
+                elif slot[0] == "range":
+                    parts.append((float(vals[g * nnat + slot[1]]), float(vals[g * nnat + slot[2]])))
                 elif a.func in ("COUNT", "SUMLONG"):
                     parts.append(int(vals_i[g * nnat + slot[1]]))
                 else:
@@ -348,6 +350,8 @@ class ServerQueryExecutor:
             for a in qc.aggregations:
                 if a.func == "AVG":
                     agg_slots.append(("avg", add("SUM", a.column, a.expr), add("COUNT", "*")))
+                elif a.func == "MINMAXRANGE":  # MinMaxRangePair = (MIN, MAX) accumulators
+                    agg_slots.append(("range", add("MIN", a.column, a.expr), add("MAX", a.column, a.expr)))
                 else:
                     agg_slots.append(("direct", add(a.func, a.column, a.expr)))
             if not qc.aggregations and qc.group_by:

@@ -13,7 +13,7 @@ import dataclasses
 import re
 from typing import List, Optional, Sequence, Tuple
 
-AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG")
+AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG", "MINMAXRANGE")
 DEFAULT_GROUP_BY_LIMIT = 10          # Pinot's default LIMIT for group-by results
 DEFAULT_NUM_GROUPS_LIMIT = 100_000   # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
 
@@ -108,7 +108,7 @@ class Aggregation:
     expr: None for a plain column, else (op, column_a, column_b) with op MUL / SUB / ADD
     (MultiplicationTransformFunction / SubtractionTransformFunction / AdditionTransformFunction;
     CAST(x AS DOUBLE) operands are accepted: every transform already computes in double)."""
-    func: str          # COUNT SUM MIN MAX AVG SUMLONG
+    func: str          # COUNT SUM MIN MAX AVG SUMLONG MINMAXRANGE
     column: str
     alias: Optional[str] = None
     expr: Optional[Tuple[str, str, str]] = None
@@ -408,10 +408,14 @@ def parse_sql(sql: str) -> QueryContext:
 
 # ---------------------------------------------------------------------------------------- reduce
 def final_value(func: str, partial):
-    """AggregationFunction.extractFinalResult: AVG -> sum / count, others unchanged."""
+    """AggregationFunction.extractFinalResult: AVG -> sum / count, MINMAXRANGE -> max - min
+    (MinMaxRangeAggregationFunction: MinMaxRangePair(+inf, -inf) when no doc matched), others unchanged."""
     if func == "AVG":
         s, c = partial
         return s / c if c else float("-inf")
+    if func == "MINMAXRANGE":
+        mn, mx = partial
+        return mx - mn
     return partial
 
 
@@ -425,6 +429,8 @@ def merge_partial(func: str, a, b):
         return max(a, b)
     if func == "AVG":
         return (a[0] + b[0], a[1] + b[1])
+    if func == "MINMAXRANGE":
+        return (min(a[0], b[0]), max(a[1], b[1]))
     raise ValueError(func)
 
 
