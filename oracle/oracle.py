@@ -20,7 +20,8 @@ from typing import Dict, List, Sequence
 
 import numpy as np
 
-from pinot_amd.query import QueryContext, merge_partial, parse_sql, reduce_rows
+from pinot_amd.query import (QueryContext, fold_distinct_count, merge_partial, parse_sql, reduce_rows,
+                             split_distinct_count)
 from pinot_amd.segment import (DOUBLE, FLOAT, INT, LONG, STRING, ColumnBuffers, SegmentBuffers,
                                parse_raw_fwd_header)
 
@@ -356,6 +357,10 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
     maps key tuple -> intermediate results per aggregation (AVG as (sum, count)), combined across
     segments with AggregationFunction.merge semantics."""
     qc = parse_sql(query) if isinstance(query, str) else query
+    if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):  # per-group value sets (query.py)
+        base, subs = split_distinct_count(qc)
+        total, bg = execute(base, segments, use_inverted)
+        return total, fold_distinct_count(qc, bg, [(i, execute(sq, segments, use_inverted)[1]) for i, sq in subs])
     total = 0
     groups: Dict[tuple, list] = {}
     for seg in segments:

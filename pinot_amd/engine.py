@@ -24,7 +24,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import ColumnSpec, PredicateSpec, check, lib
-from .query import QueryContext, parse_sql, reduce_rows
+from .query import QueryContext, fold_distinct_count, parse_sql, reduce_rows, split_distinct_count
 from .segment import ColumnBuffers, SegmentBuffers, DOUBLE, FLOAT, INT, LONG, STRING
 
 TYPE_CODE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3, STRING: 4}
@@ -153,6 +153,29 @@ def _predicate_spec(pred, column: ColumnBuffers, use_inverted: bool, keep: list)
         keep.append(arr)
         s.h_values_d = arr
     return s
+
+
+class DistinctCountResult:
+    """Result of a query with DISTINCTCOUNT aggregations (query.split_distinct_count): the base
+    result plus one grouped result per DISTINCTCOUNT, folded into per-group value sets."""
+
+    def __init__(self, qc, base, subs):
+        self.qc, self._base, self._subs = qc, base, subs
+
+    def num_docs_matched(self) -> int:
+        return self._base.num_docs_matched()
+
+    def num_groups_limit_reached(self) -> bool:
+        return self._base.num_groups_limit_reached()
+
+    def kernel_info(self) -> str:
+        return self._base.kernel_info()
+
+    def groups(self):
+        return fold_distinct_count(self.qc, self._base.groups(), [(i, r.groups()) for i, r in self._subs])
+
+    def rows(self):
+        return reduce_rows(self.qc, self.groups())
 
 
 class QueryResult:
@@ -309,8 +332,15 @@ class ServerQueryExecutor:
             raise
         return qh
 
-    def execute(self, query, segments: Sequence[ImmutableSegment], stream=None) -> QueryResult:
+    def execute(self, query, segments: Sequence[ImmutableSegment], stream=None):
         qc = parse_sql(query) if isinstance(query, str) else query
+        if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):
+            base, subs = split_distinct_count(qc)
+            return DistinctCountResult(qc, self._execute(base, segments, stream),
+                                       [(i, self._execute(sq, segments, stream)) for i, sq in subs])
+        return self._execute(qc, segments, stream)
+
+    def _execute(self, qc, segments: Sequence[ImmutableSegment], stream=None) -> QueryResult:
         if not segments:
             raise ValueError("no segments")
         L = lib()

@@ -13,7 +13,7 @@ import dataclasses
 import re
 from typing import List, Optional, Sequence, Tuple
 
-AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG", "MINMAXRANGE")
+AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG", "MINMAXRANGE", "DISTINCTCOUNT")
 DEFAULT_GROUP_BY_LIMIT = 10          # Pinot's default LIMIT for group-by results
 DEFAULT_NUM_GROUPS_LIMIT = 100_000   # InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT
 
@@ -108,7 +108,7 @@ class Aggregation:
     expr: None for a plain column, else (op, column_a, column_b) with op MUL / SUB / ADD
     (MultiplicationTransformFunction / SubtractionTransformFunction / AdditionTransformFunction;
     CAST(x AS DOUBLE) operands are accepted: every transform already computes in double)."""
-    func: str          # COUNT SUM MIN MAX AVG SUMLONG MINMAXRANGE
+    func: str          # COUNT SUM MIN MAX AVG SUMLONG MINMAXRANGE DISTINCTCOUNT
     column: str
     alias: Optional[str] = None
     expr: Optional[Tuple[str, str, str]] = None
@@ -416,6 +416,8 @@ def final_value(func: str, partial):
     if func == "MINMAXRANGE":
         mn, mx = partial
         return mx - mn
+    if func == "DISTINCTCOUNT":
+        return len(partial)
     return partial
 
 
@@ -431,7 +433,48 @@ def merge_partial(func: str, a, b):
         return (a[0] + b[0], a[1] + b[1])
     if func == "MINMAXRANGE":
         return (min(a[0], b[0]), max(a[1], b[1]))
+    if func == "DISTINCTCOUNT":
+        return a | b
     raise ValueError(func)
+
+
+# ------------------------------------------------------------------------------- DISTINCTCOUNT
+def split_distinct_count(qc: QueryContext):
+    """DistinctCountAggregationFunction keeps, per group, the set of distinct values of its column
+    among the matching docs (intermediate = the set, merge = union, final = its size). Planned as
+    device queries: the query without its DISTINCTCOUNTs (or COUNT(*) if nothing else is left), and
+    per DISTINCTCOUNT(c) the same filter grouped by (group-by columns..., c) — each distinct c of a
+    group is one group of that query. Returns (base query, [(aggregation index, sub query)])."""
+    rest = [a for a in qc.aggregations if a.func != "DISTINCTCOUNT"]
+    base = dataclasses.replace(qc, aggregations=rest or [Aggregation("COUNT", "*")], order_by=[])
+    subs = []
+    for i, a in enumerate(qc.aggregations):
+        if a.func == "DISTINCTCOUNT":
+            if a.expr is not None or a.column == "*":
+                raise ValueError("DISTINCTCOUNT takes one column")
+            subs.append((i, dataclasses.replace(qc, aggregations=[Aggregation("COUNT", "*")], order_by=[],
+                                                group_by=list(qc.group_by) + [a.column],
+                                                num_groups_limit=max(qc.num_groups_limit, 1 << 30))))
+    return base, subs
+
+
+def fold_distinct_count(qc: QueryContext, base_groups: dict, sub_groups: Sequence[Tuple[int, dict]]) -> dict:
+    """Groups of the original query from split_distinct_count's results (same group keys as the
+    base query: a group exists iff a doc matched, in every one of the queries alike)."""
+    sets = {i: {} for i, _ in sub_groups}
+    for i, g in sub_groups:
+        for key in g:
+            sets[i].setdefault(tuple(key[:-1]), set()).add(key[-1])
+    rest_idx = [j for j, a in enumerate(qc.aggregations) if a.func != "DISTINCTCOUNT"]
+    out = {}
+    for key, parts in base_groups.items():
+        full = [None] * len(qc.aggregations)
+        for j, p in zip(rest_idx, parts):
+            full[j] = p
+        for i in sets:
+            full[i] = frozenset(sets[i].get(tuple(key), ()))
+        out[key] = full
+    return out
 
 
 def reduce_rows(qc: QueryContext, groups: dict) -> List[tuple]:

@@ -550,3 +550,21 @@ def test_group_by_raw_high_cardinality(engine, kernel_mode):
         res = ex.execute(q, [seg])
         check_mode(res, kernel_mode)
         assert_same_groups(res.groups(), og)
+
+
+def test_distinct_count_vs_oracle(engine, kernel_mode):
+    """DISTINCTCOUNT (DistinctCountAggregationFunction: per-group value set, union on merge) over a
+    dictionary column and a raw column, alone and next to other aggregations, with and without GROUP BY,
+    across segments with different dictionaries."""
+    rng = np.random.default_rng(91)
+    bufs = [random_segment(rng, n, name=f"dc{i}") for i, n in enumerate([20_000, 7_001])]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    ex = engine.ServerQueryExecutor()
+    for q in ["SELECT DISTINCTCOUNT(d0), DISTINCTCOUNT(r_int) FROM t WHERE d1 < 100",
+              "SELECT d1, DISTINCTCOUNT(d0), SUM(r_long), COUNT(*) FROM t WHERE r_int > 0 GROUP BY d1",
+              "SELECT d1, DISTINCTCOUNT(r_int) FROM t GROUP BY d1"]:
+        res = ex.execute(q, segs)
+        check_mode(res, kernel_mode)
+        nm, og = oracle.execute(q, bufs)
+        assert res.num_docs_matched() == nm
+        assert res.groups() == og, q
