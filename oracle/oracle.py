@@ -86,10 +86,10 @@ def lib():
         L.oracle_filter.argtypes = [C.POINTER(OColumn), I64, C.POINTER(OLeaf), C.c_int32, P]
         L.oracle_bitset_to_doc_ids.restype = I64
         L.oracle_bitset_to_doc_ids.argtypes = [P, I64, P]
-        L.oracle_aggregate.argtypes = [C.POINTER(OColumn), I64, P, C.POINTER(OAgg), C.c_int32, P, P]
+        L.oracle_aggregate.argtypes = [C.POINTER(OColumn), I64, P, C.POINTER(OAgg), C.c_int32, P, P, P]
         L.oracle_group_by.restype = I64
-        L.oracle_group_by.argtypes = [C.POINTER(OColumn), I64, P, P, C.c_int32, C.POINTER(OAgg), C.c_int32, I64, P,
-                                      P, P]
+        L.oracle_group_by.argtypes = [C.POINTER(OColumn), I64, P, P, C.c_int32, C.POINTER(OAgg), C.c_int32, I64, I64,
+                                      P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -352,15 +352,18 @@ class OracleSegment:
         return tuple(out)
 
 
-def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True):
+def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True, stats: dict = None):
     """Run a query over segments on the CPU oracle: returns (num_docs_matched, groups) where groups
     maps key tuple -> intermediate results per aggregation (AVG as (sum, count)), combined across
-    segments with AggregationFunction.merge semantics."""
+    segments with AggregationFunction.merge semantics (GroupByCombineOperator's upsert by key).
+    stats, when given, receives 'num_groups_limit_reached' (any segment's GroupByOperator flag)."""
     qc = parse_sql(query) if isinstance(query, str) else query
     if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):  # per-group value sets (query.py)
         base, subs = split_distinct_count(qc)
-        total, bg = execute(base, segments, use_inverted)
+        total, bg = execute(base, segments, use_inverted, stats)
         return total, fold_distinct_count(qc, bg, [(i, execute(sq, segments, use_inverted)[1]) for i, sq in subs])
+    if stats is not None:
+        stats["num_groups_limit_reached"] = False
     total = 0
     groups: Dict[tuple, list] = {}
     for seg in segments:
@@ -394,43 +397,73 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
                 return OAgg(AGG[f], os_.index[c if e is None else e[1]], 0, -1)
             return OAgg(AGG[f], os_.index[e[1]], EXPR[e[0]], os_.index[e[2]])
         aggs = (OAgg * len(nat))(*[oagg(f, c, e) for f, c, e in nat])
+        int_sum = [f == "SUM" and _is_int_value(seg, c, e) for f, c, e in nat]
         bptr = _ptr(bits) if bits is not None else None
         if qc.group_by:
             cap = max(cnt, 1)
             keys = np.zeros(cap * len(qc.group_by), dtype=np.int32)
             vals = np.zeros(cap * len(nat), dtype=np.float64)
             vali = np.zeros(cap * len(nat), dtype=np.int64)
+            valh = np.zeros(cap * len(nat), dtype=np.int64)
             gcols = np.array([os_.group_col(g) for g in qc.group_by], dtype=np.int32)
-            ng = lib().oracle_group_by(os_.cols, seg.num_docs, bptr, _ptr(gcols), len(gcols), aggs, len(nat), cap,
-                                       _ptr(keys), _ptr(vals), _ptr(vali))
+            reached = C.c_int32(0)
+            ng = lib().oracle_group_by(os_.cols, seg.num_docs, bptr, _ptr(gcols), len(gcols), aggs, len(nat),
+                                       qc.num_groups_limit, cap, _ptr(keys), _ptr(vals), _ptr(vali), _ptr(valh),
+                                       C.byref(reached))
             assert ng >= 0, ng
+            if stats is not None and reached.value:
+                stats["num_groups_limit_reached"] = True
             seg_groups = {}
             for g in range(ng):
                 kv = os_.key_values(keys[g * len(qc.group_by):(g + 1) * len(qc.group_by)], qc.group_by)
-                seg_groups[kv] = _parts(qc, slots, nat, vals[g * len(nat):(g + 1) * len(nat)],
-                                        vali[g * len(nat):(g + 1) * len(nat)])
+                sl = slice(g * len(nat), (g + 1) * len(nat))
+                seg_groups[kv] = _parts(qc, slots, nat, vals[sl], vali[sl], valh[sl], int_sum)
         else:
             vals = np.zeros(len(nat), dtype=np.float64)
             vali = np.zeros(len(nat), dtype=np.int64)
-            lib().oracle_aggregate(os_.cols, seg.num_docs, bptr, aggs, len(nat), _ptr(vals), _ptr(vali))
-            seg_groups = {(): _parts(qc, slots, nat, vals, vali)}
+            valh = np.zeros(len(nat), dtype=np.int64)
+            lib().oracle_aggregate(os_.cols, seg.num_docs, bptr, aggs, len(nat), _ptr(vals), _ptr(vali), _ptr(valh))
+            seg_groups = {(): _parts(qc, slots, nat, vals, vali, valh, int_sum)}
         for k, parts in seg_groups.items():
             if k in groups:
                 groups[k] = [merge_partial(a.func, x, y) for a, x, y in zip(qc.aggregations, groups[k], parts)]
             else:
                 groups[k] = parts
+    # integer SUM partials were carried as exact Python ints through the combine: round once
+    for k, parts in groups.items():
+        groups[k] = [(float(p[0]), p[1]) if a.func == "AVG" else float(p) if a.func == "SUM" else p
+                     for a, p in zip(qc.aggregations, parts)]
     return total, groups
 
 
-def _parts(qc, slots, nat, vals, vali):
+def _is_int_value(seg: SegmentBuffers, column, expr) -> bool:
+    """agg_is_int in pinot_oracle.c: SUM over an INT/LONG column, or over times/minus/plus of two INT
+    columns, is summed exactly."""
+    if column == "*":
+        return False
+    if expr is None or expr[0] == "COL":
+        c = column if expr is None else expr[1]
+        return seg.columns[c].stored_type in (INT, LONG)
+    return seg.columns[expr[1]].stored_type == INT and seg.columns[expr[2]].stored_type == INT
+
+
+def _exact(lo, hi) -> int:
+    return (int(hi) << 64) | (int(lo) & ((1 << 64) - 1))
+
+
+def _parts(qc, slots, nat, vals, vali, valh, int_sum):
+    def sum_of(i):
+        return _exact(vali[i], valh[i]) if int_sum[i] else float(vals[i])
     out = []
     for a, s in zip(qc.aggregations, slots):
         if s[0] == "avg":
-            out.append((float(vals[s[1]]), int(vali[s[2]])))
+            out.append((sum_of(s[1]), int(vali[s[2]])))
         elif s[0] == "range":
             out.append((float(vals[s[1]]), float(vals[s[2]])))
         elif a.func in ("COUNT", "SUMLONG"):
             out.append(int(vali[s[1]]))
+        elif a.func == "SUM":
+            out.append(sum_of(s[1]))
         else:
             out.append(float(vals[s[1]]))
     return out

@@ -168,6 +168,26 @@ static double agg_f64(const oracle_column* cols, const oracle_agg* a, int64_t do
   }
 }
 
+/* Integer-valued SUM / AVG inputs (INT / LONG columns, and times/minus/plus of two INT columns) are
+ * summed exactly in 128 bits and rounded to double once. SumAggregationFunction accumulates in double
+ * (SumAggregationFunction.java:96-107,190-200); both agree whenever every partial sum stays below 2^53
+ * (true of every reference golden value), and beyond that the exact sum is the value the north star's
+ * "bit-exact integer SUM" pins (Pinot's own double accumulation then depends on the doc order). */
+static int agg_is_int(const oracle_column* cols, const oracle_agg* a) {
+  if (a->column < 0 || is_float_type(cols[a->column].stored_type)) return 0;
+  if (a->expr == OR_EXPR_COL) return 1;
+  return cols[a->column].stored_type == OR_INT && cols[a->column2].stored_type == OR_INT;
+}
+static __int128 agg_i128(const oracle_column* cols, const oracle_agg* a, int64_t doc) {
+  const __int128 x = value_i64(&cols[a->column], doc);
+  switch (a->expr) {
+    case OR_EXPR_MUL: return x * value_i64(&cols[a->column2], doc);
+    case OR_EXPR_SUB: return x - value_i64(&cols[a->column2], doc);
+    case OR_EXPR_ADD: return x + value_i64(&cols[a->column2], doc);
+    default: return x;
+  }
+}
+
 /* LZ4 block decoding as lz4-java's LZ4FastDecompressor does it (org.lz4:lz4-java 1.11.0, pom.xml:186,
  * third-party): the chunk decompressor behind ChunkCompressionType.LZ4
  * (pinot-segment-local/.../io/compression/LZ4Decompressor.java). Returns bytes written or -1. */
@@ -466,10 +486,11 @@ int64_t oracle_bitset_to_doc_ids(const uint64_t* bitset, int64_t num_docs, int32
  * (MinAggregationFunction.java:38,83-135,175-185); COUNT: long; SUMLONG: long wrap
  * (SumLongAggregationFunction.java). */
 int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset, const oracle_agg* aggs,
-                     int32_t naggs, double* out, int64_t* out_i64) {
+                     int32_t naggs, double* out, int64_t* out_i64, int64_t* out_hi64) {
   double* holder = (double*)malloc(sizeof(double) * (size_t)naggs);
   double* inner = (double*)malloc(sizeof(double) * (size_t)naggs);
   int64_t* li = (int64_t*)calloc((size_t)naggs, sizeof(int64_t));
+  __int128* exact = (__int128*)calloc((size_t)naggs, sizeof(__int128));
   for (int32_t a = 0; a < naggs; a++) {
     holder[a] = aggs[a].func == OR_AGG_MIN ? INFINITY : aggs[a].func == OR_AGG_MAX ? -INFINITY : 0.0;
   }
@@ -490,6 +511,10 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
           li[a] += len;
           break;
         case OR_AGG_SUM: {
+          if (agg_is_int(cols, &aggs[a])) {  /* exact, see agg_is_int */
+            for (int32_t i = 0; i < len; i++) exact[a] += agg_i128(cols, &aggs[a], block[i]);
+            break;
+          }
           double s = 0;
           for (int32_t i = 0; i < len; i++) s += agg_f64(cols, &aggs[a], block[i]);
           holder[a] = s + holder[a];
@@ -525,162 +550,167 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
     if (aggs[a].func == OR_AGG_COUNT || aggs[a].func == OR_AGG_SUMLONG) {
       out[a] = (double)li[a];
       out_i64[a] = li[a];
+      out_hi64[a] = li[a] < 0 ? -1 : 0;
+    } else if (aggs[a].func == OR_AGG_SUM && agg_is_int(cols, &aggs[a])) {
+      out[a] = (double)exact[a];
+      out_i64[a] = (int64_t)(uint64_t)(unsigned __int128)exact[a];
+      out_hi64[a] = (int64_t)(exact[a] >> 64);
     } else {
       out[a] = holder[a];
       out_i64[a] = 0;
+      out_hi64[a] = 0;
     }
   }
   free(holder);
   free(inner);
   free(li);
+  free(exact);
   return 0;
 }
 
 /* ------------------------------------------------------------------ group-by */
 
 typedef struct {
-  const int32_t* ids; /* dictIds of the doc's group-by columns */
-  int64_t doc;
-} key_doc;
+  double h;        /* double holder (SUM on floating values, MIN, MAX) */
+  int64_t li;      /* COUNT / SUMLONG */
+  __int128 exact;  /* SUM on integer values */
+} or_holder;
 
-static int g_ngroup; /* qsort has no context argument */
-
-/* order of DictionaryBasedGroupKeyGenerator raw keys: column n-1 most significant */
-static int cmp_key_doc(const void* a, const void* b) {
-  const key_doc* x = (const key_doc*)a;
-  const key_doc* y = (const key_doc*)b;
-  for (int32_t j = g_ngroup - 1; j >= 0; j--)
-    if (x->ids[j] != y->ids[j]) return x->ids[j] < y->ids[j] ? -1 : 1;
-  return x->doc < y->doc ? -1 : (x->doc > y->doc);
+static void holder_init(or_holder* h, int func) {
+  h->h = func == OR_AGG_MIN ? INFINITY : func == OR_AGG_MAX ? -INFINITY : 0.0;
+  h->li = 0;
+  h->exact = 0;
 }
 
-/* DictionaryBasedGroupKeyGenerator raw keys: key = sum_j dictId_j * prod_{i<j} card_i, i.e. the
- * loop `rawKey = rawKey * card[j] + dictId[j]` for j = n-1..0
- * (pinot-core/.../aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:316-327,427-434); beyond
- * the long range the ARRAY_MAP_BASED holder keys on the dictId array itself (same grouping), so the
- * oracle groups on the dictId tuple and emits it (out_keys[g*ngroup + j]).
- * Per group, docs are folded in docId order with the group-by semantics of each function:
+/* DefaultGroupByExecutor.process -> AggregationFunction.aggregateGroupBySV for one doc of a group:
  * SUM: holder + value (SumAggregationFunction.java:190-200), MIN: `value < holder`
  * (MinAggregationFunction.java:215-223), MAX: `value > holder`, COUNT: +1, SUMLONG: long wrap. */
+static void holder_add(or_holder* h, const oracle_column* cols, const oracle_agg* a, int64_t doc) {
+  const oracle_column* c = a->column >= 0 ? &cols[a->column] : NULL;
+  switch (a->func) {
+    case OR_AGG_COUNT: h->li += 1; break;
+    case OR_AGG_SUM:
+      if (agg_is_int(cols, a)) h->exact += agg_i128(cols, a, doc);
+      else h->h = h->h + agg_f64(cols, a, doc);
+      break;
+    case OR_AGG_SUMLONG: h->li = (int64_t)((uint64_t)h->li + (uint64_t)value_i64(c, doc)); break;
+    case OR_AGG_MIN: { double v = agg_f64(cols, a, doc); if (v < h->h) h->h = v; break; }
+    case OR_AGG_MAX: { double v = agg_f64(cols, a, doc); if (v > h->h) h->h = v; break; }
+  }
+}
+
+/* out: the double result; out_i / out_hi: COUNT / SUMLONG as int64 (sign-extended), and an integer
+ * SUM's exact 128-bit value as (low, high) words, so the combine can carry it exactly */
+static void holder_out(const or_holder* h, const oracle_column* cols, const oracle_agg* a, double* out, int64_t* out_i,
+                       int64_t* out_hi) {
+  *out_hi = 0;
+  switch (a->func) {
+    case OR_AGG_COUNT:
+    case OR_AGG_SUMLONG: *out = (double)h->li; *out_i = h->li; *out_hi = h->li < 0 ? -1 : 0; break;
+    case OR_AGG_SUM:
+      if (agg_is_int(cols, a)) {
+        *out = (double)h->exact;
+        *out_i = (int64_t)(uint64_t)(unsigned __int128)h->exact;
+        *out_hi = (int64_t)(h->exact >> 64);
+      } else {
+        *out = h->h;
+        *out_i = 0;
+      }
+      break;
+    default: *out = h->h; *out_i = 0;
+  }
+}
+
+static uint64_t mix_ids(const int32_t* ids, int32_t n) {
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (int32_t j = 0; j < n; j++) {
+    x ^= (uint64_t)(uint32_t)ids[j];
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+  }
+  return x;
+}
+
+/* GroupByOperator + DefaultGroupByExecutor + DictionaryBasedGroupKeyGenerator over one segment.
+ * Raw keys: key = sum_j dictId_j * prod_{i<j} card_i (the loop `rawKey = rawKey * card[j] + dictId[j]`
+ * for j = n-1..0, DictionaryBasedGroupKeyGenerator.java:316-327,427-434); the holder is chosen as the
+ * constructor does (:144-180):
+ *   ARRAY_BASED when the key space is <= arrayBasedThreshold (10000) and <= numGroupsLimit: one slot
+ *     per raw key, every key admitted (:304-342);
+ *   otherwise a map holder (IntMapBasedHolder / LongMapBasedHolder / ArrayMapBasedHolder, :444-900),
+ *     all with getGroupId(rawKey, numGroupsLimit) semantics: a key absent from the map gets the next
+ *     group id while the map holds fewer than numGroupsLimit keys, and is dropped (INVALID_ID) after
+ *     that (:651-659). Docs are visited in docId order, so a segment keeps the first numGroupsLimit
+ *     keys its matching docs reach. Keyed here on the dictId tuple itself (the raw key is a bijection
+ *     of it).
+ * out_keys[g*ngroup + j] = dictId of group-by column j; groups in group-id order. *out_limit_reached =
+ * numGroups >= numGroupsLimit (GroupByOperator.java:133). Returns groups, or -1 beyond max_groups. */
 int64_t oracle_group_by(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset,
                         const int32_t* group_cols, int32_t ngroup, const oracle_agg* aggs, int32_t naggs,
-                        int64_t max_groups, int32_t* out_keys, double* out_vals, int64_t* out_i64) {
-  /* ARRAY_BASED holder (DictionaryBasedGroupKeyGenerator.java:144-152,304-342): when the raw key
-   * space is at most arrayBasedThreshold (10000), the raw key is the group id — one array slot per
-   * possible key, docs folded in docId order. */
+                        int64_t num_groups_limit, int64_t max_groups, int32_t* out_keys, double* out_vals,
+                        int64_t* out_i64, int64_t* out_hi64, int32_t* out_limit_reached) {
   double prod = 1;
   for (int32_t j = 0; j < ngroup; j++) prod *= (double)cols[group_cols[j]].cardinality;
-  if (prod <= 10000) {
-    int64_t nkeys = (int64_t)prod;
-    double* hv = (double*)malloc(sizeof(double) * (size_t)(nkeys * naggs));
-    int64_t* hi = (int64_t*)calloc((size_t)(nkeys * naggs), sizeof(int64_t));
-    int64_t* cnt = (int64_t*)calloc((size_t)nkeys, sizeof(int64_t));
-    for (int64_t k = 0; k < nkeys; k++)
-      for (int32_t a = 0; a < naggs; a++)
-        hv[k * naggs + a] = aggs[a].func == OR_AGG_MIN ? INFINITY : aggs[a].func == OR_AGG_MAX ? -INFINITY : 0.0;
-    for (int64_t d = 0; d < num_docs; d++) {
-      if (bitset && !((bitset[d >> 6] >> (d & 63)) & 1)) continue;
-      int64_t key = 0;
-      for (int32_t j = ngroup - 1; j >= 0; j--) key = key * cols[group_cols[j]].cardinality + dict_id_of(&cols[group_cols[j]], d);
-      cnt[key]++;
-      for (int32_t a = 0; a < naggs; a++) {
-        const oracle_column* c = aggs[a].column >= 0 ? &cols[aggs[a].column] : NULL;
-        double* h = &hv[key * naggs + a];
-        int64_t* li = &hi[key * naggs + a];
-        switch (aggs[a].func) {
-          case OR_AGG_COUNT: *li += 1; *h = (double)*li; break;
-          case OR_AGG_SUM: *h = *h + agg_f64(cols, &aggs[a], d); break;
-          case OR_AGG_SUMLONG: *li = (int64_t)((uint64_t)*li + (uint64_t)value_i64(c, d)); *h = (double)*li; break;
-          case OR_AGG_MIN: { double v = agg_f64(cols, &aggs[a], d); if (v < *h) *h = v; break; }
-          case OR_AGG_MAX: { double v = agg_f64(cols, &aggs[a], d); if (v > *h) *h = v; break; }
-        }
-      }
-    }
-    int64_t g = 0;
-    for (int64_t k = 0; k < nkeys; k++) {
-      if (!cnt[k]) continue;
-      if (g >= max_groups) { g = -1; break; }
-      int64_t rem = k;
-      for (int32_t j = 0; j < ngroup; j++) {
-        out_keys[g * ngroup + j] = (int32_t)(rem % cols[group_cols[j]].cardinality);
-        rem /= cols[group_cols[j]].cardinality;
-      }
-      for (int32_t a = 0; a < naggs; a++) {
-        out_vals[g * naggs + a] = hv[k * naggs + a];
-        out_i64[g * naggs + a] = hi[k * naggs + a];
-      }
-      g++;
-    }
-    free(hv);
-    free(hi);
-    free(cnt);
-    return g;
-  }
+  const int array_based = prod <= 10000 && prod <= (double)num_groups_limit;
   int64_t nmatch = 0;
   for (int64_t d = 0; d < num_docs; d++)
     if (!bitset || ((bitset[d >> 6] >> (d & 63)) & 1)) nmatch++;
-  key_doc* kd = (key_doc*)malloc(sizeof(key_doc) * (size_t)(nmatch ? nmatch : 1));
-  int32_t* ids = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nmatch ? nmatch : 1) * (size_t)(ngroup ? ngroup : 1));
-  int64_t n = 0;
+  /* group ids -> keys and holders */
+  const int64_t max_ids = array_based ? (int64_t)prod : (nmatch < num_groups_limit ? nmatch : num_groups_limit);
+  int32_t* gkeys = (int32_t*)malloc(sizeof(int32_t) * (size_t)(max_ids + 1) * (size_t)(ngroup ? ngroup : 1));
+  or_holder* hold = (or_holder*)malloc(sizeof(or_holder) * (size_t)(max_ids + 1) * (size_t)(naggs ? naggs : 1));
+  int64_t* array_gid = NULL;  /* ARRAY_BASED: raw key -> group id */
+  int64_t* slots = NULL;      /* map holder: open addressing over group ids */
+  int64_t cap = 16;
+  if (array_based) {
+    array_gid = (int64_t*)malloc(sizeof(int64_t) * (size_t)(prod > 0 ? prod : 1));
+    for (int64_t k = 0; k < (int64_t)prod; k++) array_gid[k] = -1;
+  } else {
+    while (cap < 2 * max_ids + 16) cap <<= 1;
+    slots = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap);
+    for (int64_t i = 0; i < cap; i++) slots[i] = -1;
+  }
+  int64_t ngroups = 0;
+  int32_t ids[64];
   for (int64_t d = 0; d < num_docs; d++) {
     if (bitset && !((bitset[d >> 6] >> (d & 63)) & 1)) continue;
-    int32_t* row = ids + n * ngroup;
-    for (int32_t j = 0; j < ngroup; j++) row[j] = dict_id_of(&cols[group_cols[j]], d);
-    kd[n].ids = row;
-    kd[n].doc = d;
-    n++;
-  }
-  g_ngroup = ngroup;
-  qsort(kd, (size_t)n, sizeof(key_doc), cmp_key_doc);
-  int64_t g = -1;
-  for (int64_t i = 0; i < n; i++) {
-    int newgroup = i == 0;
-    for (int32_t j = 0; j < ngroup && !newgroup; j++) newgroup = kd[i].ids[j] != kd[i - 1].ids[j];
-    if (newgroup) {
-      g++;
-      if (g >= max_groups) {
-        free(kd);
-        free(ids);
-        return -1;
+    for (int32_t j = 0; j < ngroup; j++) ids[j] = dict_id_of(&cols[group_cols[j]], d);
+    int64_t gid = -1;
+    if (array_based) {
+      int64_t key = 0;
+      for (int32_t j = ngroup - 1; j >= 0; j--) key = key * cols[group_cols[j]].cardinality + ids[j];
+      gid = array_gid[key];
+      if (gid < 0) gid = array_gid[key] = ngroups++;
+      else goto have;
+    } else {
+      uint64_t i = mix_ids(ids, ngroup) & (uint64_t)(cap - 1);
+      for (;; i = (i + 1) & (uint64_t)(cap - 1)) {
+        if (slots[i] < 0) break;
+        if (memcmp(&gkeys[slots[i] * ngroup], ids, sizeof(int32_t) * (size_t)ngroup) == 0) { gid = slots[i]; goto have; }
       }
-      for (int32_t j = 0; j < ngroup; j++) out_keys[g * ngroup + j] = kd[i].ids[j];
-      for (int32_t a = 0; a < naggs; a++) {
-        int f = aggs[a].func;
-        out_vals[g * naggs + a] = f == OR_AGG_MIN ? INFINITY : f == OR_AGG_MAX ? -INFINITY : 0.0;
-        out_i64[g * naggs + a] = 0;
-      }
+      if (ngroups >= num_groups_limit) continue;  /* INVALID_ID: the doc's key is not admitted */
+      gid = slots[i] = ngroups++;
     }
-    int64_t doc = kd[i].doc;
-    for (int32_t a = 0; a < naggs; a++) {
-      const oracle_column* c = aggs[a].column >= 0 ? &cols[aggs[a].column] : NULL;
-      double* h = &out_vals[g * naggs + a];
-      int64_t* hi = &out_i64[g * naggs + a];
-      switch (aggs[a].func) {
-        case OR_AGG_COUNT:
-          *hi += 1;
-          *h = (double)*hi;
-          break;
-        case OR_AGG_SUM:
-          *h = *h + agg_f64(cols, &aggs[a], doc);
-          break;
-        case OR_AGG_SUMLONG:
-          *hi = (int64_t)((uint64_t)*hi + (uint64_t)value_i64(c, doc));
-          *h = (double)*hi;
-          break;
-        case OR_AGG_MIN: {
-          double v = agg_f64(cols, &aggs[a], doc);
-          if (v < *h) *h = v;
-          break;
-        }
-        case OR_AGG_MAX: {
-          double v = agg_f64(cols, &aggs[a], doc);
-          if (v > *h) *h = v;
-          break;
-        }
-      }
+    memcpy(&gkeys[gid * ngroup], ids, sizeof(int32_t) * (size_t)ngroup);
+    for (int32_t a = 0; a < naggs; a++) holder_init(&hold[gid * naggs + a], aggs[a].func);
+  have:
+    for (int32_t a = 0; a < naggs; a++) holder_add(&hold[gid * naggs + a], cols, &aggs[a], d);
+  }
+  if (out_limit_reached) *out_limit_reached = ngroups >= num_groups_limit;
+  int64_t ret = ngroups;
+  if (ngroups > max_groups) {
+    ret = -1;
+  } else {
+    for (int64_t g = 0; g < ngroups; g++) {
+      for (int32_t j = 0; j < ngroup; j++) out_keys[g * ngroup + j] = gkeys[g * ngroup + j];
+      for (int32_t a = 0; a < naggs; a++)
+        holder_out(&hold[g * naggs + a], cols, &aggs[a], &out_vals[g * naggs + a], &out_i64[g * naggs + a],
+                   &out_hi64[g * naggs + a]);
     }
   }
-  free(kd);
-  free(ids);
-  return g + 1;
+  free(gkeys);
+  free(hold);
+  free(array_gid);
+  free(slots);
+  return ret;
 }

@@ -94,17 +94,20 @@ int64_t oracle_filter(const oracle_column* cols, int64_t num_docs, const oracle_
 int64_t oracle_bitset_to_doc_ids(const uint64_t* bitset, int64_t num_docs, int32_t* out);
 
 /* ---- aggregation (AggregationOperator) ---- */
-/* out: per agg one double (COUNT as double too), out_i64: per agg one int64 (COUNT/SUMLONG exact) */
+/* out: per agg one double (COUNT as double too); out_i64 / out_hi64: COUNT / SUMLONG as int64, and an
+ * integer SUM's exact 128-bit value as (low, high) words */
 int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset, const oracle_agg* aggs,
-                     int32_t naggs, double* out, int64_t* out_i64);
+                     int32_t naggs, double* out, int64_t* out_i64, int64_t* out_hi64);
 
 /* ---- group-by (GroupByOperator + DefaultGroupByExecutor + DictionaryBasedGroupKeyGenerator) ---- */
-/* Groups are emitted in raw-key order (mixed radix of dictIds, column 0 least significant);
- * out_keys[g*ngroup + j] = dictId of group-by column j; out_vals[g*naggs + a]; out_i64 likewise for
- * COUNT/SUMLONG. Returns number of groups or -1 if more than max_groups. */
+/* Groups in group-id (first-seen) order, at most num_groups_limit of them (the map holders' trimming);
+ * out_keys[g*ngroup + j] = dictId of group-by column j; out_vals[g*naggs + a]; out_i64 / out_hi64 as
+ * in oracle_aggregate. *out_limit_reached = numGroupsLimitReached.
+ * Returns number of groups or -1 if more than max_groups. */
 int64_t oracle_group_by(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset,
                         const int32_t* group_cols, int32_t ngroup, const oracle_agg* aggs, int32_t naggs,
-                        int64_t max_groups, int32_t* out_keys, double* out_vals, int64_t* out_i64);
+                        int64_t num_groups_limit, int64_t max_groups, int32_t* out_keys, double* out_vals,
+                        int64_t* out_i64, int64_t* out_hi64, int32_t* out_limit_reached);
 
 #ifdef __cplusplus
 }

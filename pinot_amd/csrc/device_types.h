@@ -8,11 +8,12 @@ namespace pamd {
 constexpr int kBlock = 256;                         // 4 waves of 64
 constexpr int kDocsPerThread = 4;                   // 4 consecutive docs per lane
 constexpr int kTileDocs = kBlock * kDocsPerThread;  // 1024 docs per block-tile
-constexpr int kMaxSlots = 8;                        // distinct columns referenced by one query
+constexpr int kMaxSlots = 16;                       // distinct columns referenced by one query
 constexpr int kMaxLeaves = 16;                      // predicate leaves
 constexpr int kMaxClauses = 16;                     // CNF clauses (4 bits each in a 64-bit word)
-constexpr int kMaxAcc = 10;                         // accumulator arrays (acc 0 = COUNT)
-constexpr int kMaxGroupCols = 4;
+constexpr int kMaxAcc = 16;                         // accumulator arrays (acc 0 = COUNT)
+constexpr int kMaxGroupCols = 16;
+constexpr int kMaxKeyWords = 8;                     // 64-bit words of a hash-table group key
 // slack the kernels may read past the end of a column buffer (5 dwords of a bit window, a 32 B
 // value vector of the last tile)
 constexpr int kPadBytes = kTileDocs * 8 + 256;
@@ -36,7 +37,12 @@ enum : int32_t {
 };
 
 // accumulator ops
-enum : int32_t { ACC_COUNT = 0, ACC_SUM_I64 = 1, ACC_SUM_F64 = 2, ACC_MIN = 3, ACC_MAX = 4 };
+//   ACC_SUM_I64   wrapping int64 sum (SUMLONG: Java long arithmetic)
+//   ACC_SUM_I128  exact sum of int64 values: low word here, high word in the next array (ACC_HI),
+//                 carried with the value returned by the low word's atomic (SUM / AVG on integers)
+//   ACC_FIRST_DOC smallest matching docId of a (segment, key) entry (numGroupsLimit trimming)
+enum : int32_t { ACC_COUNT = 0, ACC_SUM_I64 = 1, ACC_SUM_F64 = 2, ACC_MIN = 3, ACC_MAX = 4, ACC_SUM_I128 = 5,
+                 ACC_HI = 6, ACC_FIRST_DOC = 7 };
 
 struct DevColumn {
   const uint8_t* data;     // FIXED_BIT: BE bit stream | RAW: BE values | SORTED: LE int32 start docId per dictId
@@ -57,7 +63,9 @@ struct DevLeaf {
 
 struct DevSegment {
   int64_t num_docs;
-  int64_t tile_begin;      // first global tile of this segment
+  int64_t tile_begin;      // first tile of this segment in its launch
+  int32_t key_seg;         // index of the segment in its trim batch (hash key word of trimming plans)
+  int32_t pad;
   DevColumn cols[kMaxSlots];
   DevLeaf leaves[kMaxLeaves];
 };
@@ -107,20 +115,26 @@ struct ChunkJob {
   int32_t codec, pad;
 };
 
-// Uniform per-launch plan. Leaves and accumulators are grouped by the slot they read so the
-// kernel's per-slot loop indexes the decoded values with compile-time indices only.
+// Hash-table group-by (key spaces a dense table cannot hold, and numGroupsLimit trimming): open
+// addressing with linear probing over `cap` slots. A key is `nwords` 64-bit words (the group columns'
+// merged ids packed <= 63 bits per word, so no word is ever ~0; trimming plans add the batch segment
+// index as the last word), stored word-major at keys[w * cap + slot]; EMPTY words are ~0. A slot is
+// claimed word by word with compare-and-swap: whoever sets word w decides it, a thread finding a
+// different word moves on to the next slot, so a slot's key is complete once every thread that
+// touched it has passed (no locks, no spinning). Accumulators live at acc[a * cap + slot].
+struct DevHash {
+  unsigned long long* keys;
+  int64_t cap;                       // power of two
+  unsigned long long* overflow;      // docs that found no free slot (the host fails the query if > 0)
+};
+
+// Uniform per-launch plan (kernel argument of the generated scan kernels and the fixed passes).
 struct DevQuery {
-  int32_t nsegs, nslots, nleaves, nclauses;
-  int32_t slot_leaf_begin[kMaxSlots + 1];   // leaves of slot s: [begin[s], begin[s+1]); docId leaves after
-  int32_t slotless_leaf_begin, slotless_leaf_end;
-  int32_t slot_acc_begin[kMaxSlots + 1];    // accumulators fed by slot s
-  int64_t slot_group_stride[kMaxSlots];     // > 0: slot is a group-by column with this key stride
+  int32_t nsegs;                            // segments of this launch (DevSegment array length)
   int32_t nacc;                             // accumulator arrays, acc 0 = COUNT
   int32_t acc_op[kMaxAcc];
-  int32_t lds_keys;                         // > 0: LDS-privatised table of lds_keys keys
-  int32_t agg_only;                         // no GROUP BY: MIN/MAX propagate NaN (Math.min/max)
-  int64_t num_keys;                         // dense key space (1 for aggregation only)
-  int64_t total_tiles;
+  int64_t num_keys;                         // dense key space (1 for aggregation only; hash plans: 0)
+  int64_t total_tiles;                      // 1024-doc tiles of this launch
 };
 
 }  // namespace pamd

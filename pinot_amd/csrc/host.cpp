@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <map>
 #include <memory>
@@ -25,10 +26,18 @@
 #include "jit.h"
 
 namespace pamd {
-hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
-                       unsigned long long* d_matched, int grid, hipStream_t st);
-hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st);
-int scan_blocks_per_cu(int nslots, bool lds, size_t shmem);
+hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st);
+hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc, int fd_acc,
+                       int32_t nsegs, int64_t limit, const int64_t* bucket_base, uint32_t* hist,
+                       unsigned long long* seg_distinct, int64_t* bstar, int64_t* rank, unsigned long long* bitmap,
+                       int64_t* dstar, unsigned long long* limit_reached, hipStream_t st);
+hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int nw, int has_seg, const uint64_t* sacc,
+                             unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q, int fd_acc,
+                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st);
+hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st);
+hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
+                                int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
+                                hipStream_t st);
 hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
@@ -709,12 +718,32 @@ struct MergedKeyColumn {
   size_t size() const { return type == T_STRING ? vs.size() : is_float(type) ? vd.size() : vi.size(); }
 };
 
+// One kernel launch of a plan: the segments of a batch that share a shape (every slot's encoding and
+// fixed-bit width), with their own descriptors and query-specialised kernels. Segments whose
+// columns are encoded differently (a table whose index config changed between segments) run in
+// separate launches accumulating into the same table, so every launch has compile-time decoders.
+struct Launch {
+  std::vector<int> segs;      // indices into the query's segment list
+  int batch = 0;              // hash trimming batch
+  DevQuery q{};               // nsegs / total_tiles of this launch; acc ops shared
+  DevBuf d_segs;
+  DevBuf d_bitset_ptrs;       // filter-only plans: this launch's segments' docId bitsets
+  JitKernel* jit = nullptr;         // scan, or the partitioned count / scatter / aggregate trio
+  JitKernel* jit_atomic = nullptr;  // partitioned: direct-atomic scan used when few docs match
+  JitKernel* jit_sample = nullptr;  // partitioned: match count over every sample_stride-th tile
+  int grid = 1, atomic_grid = 1, sample_grid = 1, agg_grid = 1, scan_nsub = 1;
+  size_t shmem = 0, shmem_scatter = 0, shmem_agg = 0;
+  DevPartition part{};
+  int64_t docs = 0, tiles = 0;
+};
+
+enum PlanKind { PLAN_DENSE = 0, PLAN_PARTITIONED = 1, PLAN_HASH = 2, PLAN_FILTER = 3 };
+
 struct pinot_amd_result {
   hipStream_t stream = nullptr;
-  // compiled plan
-  DevQuery q{};
-  std::vector<DevSegment> hsegs;
-  DevBuf d_segs;
+  PlanKind kind = PLAN_DENSE;
+  DevQuery q{};                  // plan-wide: nacc, acc_op, num_keys (dense)
+  std::deque<Launch> launches;  // deque: Launch holds device buffers and is never moved
   std::vector<std::unique_ptr<DevBuf>> owned;  // leaf sets, remaps, bitsets
   // inverted index leaves to (re)build each execution: (segment, leaf, container selection)
   struct InvLeaf {
@@ -729,35 +758,41 @@ struct pinot_amd_result {
   std::vector<InvLeaf> inv_leaves;
   DevBuf d_expand_jobs;        // one ExpandJob per inv_leaves entry (batched clear + expand launches)
   int64_t expand_total = 0;   // work items: (job, 65536-doc chunk) pairs
-  int grid = 1;
   std::vector<std::unique_ptr<DevBuf>> bitsets;  // filter-only plans: one docId bitset per segment
   std::vector<int64_t> bitset_words;
-  DevBuf d_bitset_ptrs;
-  DevBuf acc;
+  DevBuf acc;                  // dense table, or the hash plan's final table accumulators
+  // counters: 3 per launch ([0] count pass / scan matches, [1] sampled matches, [2] direct-atomic
+  // scan matches), then numGroupsLimitReached, then hash overflow
   DevBuf matched;
   std::vector<MergedKeyColumn> keys;  // merged dictionaries of the group-by columns
-  std::vector<int64_t> key_stride;
+  std::vector<int64_t> key_stride;    // dense: mixed-radix strides
   std::vector<int32_t> agg_acc;        // aggregation -> accumulator index (AVG: sum acc)
   std::vector<int32_t> agg_type;
   int32_t num_group_by = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double last_ms = 0;
-  JitKernel* jit = nullptr;      // query-specialised kernel (nullptr: AOT scan_kernel)
-  std::string jit_status;        // why the AOT kernel runs, if it does
-  size_t shmem = 0;
-  // partitioned GROUP BY (JIT only): count -> offsets -> scatter -> per-partition LDS aggregation
-  int64_t num_groups_limit = 100000;
-  bool partitioned = false;
-  JitKernel* jit_atomic = nullptr;  // partitioned plans: direct-atomic scan used when few docs match
-  int atomic_grid = 1;
-  JitKernel* jit_sample = nullptr;  // partitioned plans: match count over every sample_stride-th tile
-  int sample_grid = 1;
-  DevPartition part{};
+  std::string jit_status;
+  // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
-  int rec_bytes = 0, stage_cap = 0;
-  int agg_grid = 1;
-  int scan_nsub = 1;            // JIT scan: 256-thread groups per block (4: CU-wide block, large LDS table)
-  size_t shmem_scatter = 0, shmem_agg = 0;
+  // hash-table GROUP BY
+  int nw = 0;                          // key words (group columns)
+  std::vector<int> pack_word, pack_shift, pack_bits;
+  DevBuf fkeys;                        // final table keys (nw x fcap)
+  int64_t fcap = 0;
+  bool trim = false;                   // numGroupsLimit trimming (scan tables keyed by (key, segment))
+  int64_t limit = 100000;
+  bool limit_possible = false;         // some segment may hold >= numGroupsLimit keys
+  int nbatches = 1;
+  std::vector<int64_t> batch_cap;      // scan table slots per batch
+  std::vector<int32_t> batch_nsegs;
+  std::vector<int64_t> batch_bucket_off;  // offset of the batch's bucket_base array in d_bucket_base
+  std::vector<int64_t> batch_buckets;
+  DevBuf skeys, sacc;                  // trim scan table (largest batch)
+  DevBuf d_bucket_base, t_hist, t_distinct, t_bstar, t_rank, t_bitmap, t_dstar;
+  int fd_acc = -1;                     // ACC_FIRST_DOC accumulator index
+  // result compaction cache (valid until the next execution)
+  bool compacted = false;
+  int64_t ngroups = 0;
+  std::vector<uint64_t> ckeys, cacc;  // per group: key words (hash) or dense key; all accumulator words
   ~pinot_amd_result() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1194,51 +1229,114 @@ static int remap_for(const Column& c, const MergedKeyColumn& m, std::vector<int3
   return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// execution
+// ------------------------------------------------------------------------------------------------
+static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table, const DevHash& H) {
+  hipStream_t st = r->stream;
+  const DevSegment* segs = (const DevSegment*)L.d_segs.p;
+  uint64_t* const* bits = r->kind == PLAN_FILTER ? (uint64_t* const*)L.d_bitset_ptrs.p : nullptr;
+  unsigned long long* matched = (unsigned long long*)r->matched.p + 3 * li;
+  DevHash h = H;
+  void* args[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
+  if (r->kind != PLAN_PARTITIONED) {
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock * L.scan_nsub, 1, 1, (unsigned)L.shmem, st, args,
+                                 nullptr));
+    return 0;
+  }
+  const unsigned pt = (unsigned)(kBlock * kPartSub);
+  const unsigned count_grid = (unsigned)(L.grid * kPartCountRatio);
+  if (L.jit_sample) {
+    unsigned long long* sampled = matched + 1;
+    void* sargs[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&sampled, (void*)&L.part, (void*)&h};
+    HIP_OK(hipModuleLaunchKernel(L.jit_sample->fn, (unsigned)L.sample_grid, 1, 1, kBlock, 1, 1, 0, st, sargs, nullptr));
+  }
+  HIP_OK(hipModuleLaunchKernel(L.jit->fn, count_grid, 1, 1, pt, 1, 1, (unsigned)L.shmem, st, args, nullptr));
+  HIP_OK(launch_partition_offsets(L.part.hist, L.part.nparts, count_grid, L.part.offs, L.part.part_begin, st));
+  if (L.jit_atomic)
+    HIP_OK(hipModuleLaunchKernel(L.jit_atomic->fn, (unsigned)L.atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+  HIP_OK(hipModuleLaunchKernel(L.jit->fn_scatter, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem_scatter, st, args,
+                               nullptr));
+  void* agg_args[] = {(void*)&L.part, (void*)&table};
+  HIP_OK(hipModuleLaunchKernel(L.jit->fn_agg, (unsigned)L.agg_grid, 1, 1, 1024, 1, 1, (unsigned)L.shmem_agg, st,
+                               agg_args, nullptr));
+  return 0;
+}
+
 static int run_plan(pinot_amd_result* r) {
   hipStream_t st = r->stream;
-  // inverted-index leaves: expand roaring containers into dense doc bitsets
+  r->compacted = false;
   HIP_OK(hipEventRecord(r->ev0, st));
+  // inverted-index leaves: expand roaring containers into dense doc bitsets
   if (!r->inv_leaves.empty())
     HIP_OK(launch_expand_jobs(r->d_expand_jobs.p, (int32_t)r->inv_leaves.size(), r->expand_total, st));
-  HIP_OK(hipMemsetAsync(r->matched.p, 0, 3 * sizeof(unsigned long long), st));
-  if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, st));
-  if (r->jit && r->partitioned) {
-    const DevSegment* segs = (const DevSegment*)r->d_segs.p;
-    uint64_t* acc = (uint64_t*)r->acc.p;
-    uint64_t* const* bits = nullptr;
-    unsigned long long* matched = (unsigned long long*)r->matched.p;
-    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
-    const unsigned pt = (unsigned)(kBlock * kPartSub);
-    const unsigned count_grid = (unsigned)(r->grid * kPartCountRatio);
-    if (r->jit_sample) {
-      unsigned long long* sampled = matched + 1;
-      void* sargs[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&sampled, (void*)&r->part};
-      HIP_OK(hipModuleLaunchKernel(r->jit_sample->fn, (unsigned)r->sample_grid, 1, 1, kBlock, 1, 1, 0, st, sargs, nullptr));
+  HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
+  const size_t nl = r->launches.size();
+  unsigned long long* ctr = (unsigned long long*)r->matched.p;
+  unsigned long long* limit_flag = ctr + 3 * nl;
+  unsigned long long* overflow = ctr + 3 * nl + 1;
+  if (r->kind == PLAN_HASH) {
+    HIP_OK(hipMemsetAsync(r->fkeys.p, 0xFF, (size_t)r->nw * (size_t)r->fcap * 8, st));  // EMPTY key words
+    HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, r->fcap, st));
+    for (int b = 0; b < r->nbatches; ++b) {
+      DevHash H{};
+      uint64_t* table;
+      if (r->trim) {
+        const int64_t cap = r->batch_cap[b];
+        HIP_OK(hipMemsetAsync(r->skeys.p, 0xFF, (size_t)(r->nw + 1) * (size_t)cap * 8, st));
+        HIP_OK(launch_init_acc((uint64_t*)r->sacc.p, r->q, cap, st));
+        H.keys = (unsigned long long*)r->skeys.p;
+        H.cap = cap;
+        table = (uint64_t*)r->sacc.p;
+      } else {
+        H.keys = (unsigned long long*)r->fkeys.p;
+        H.cap = r->fcap;
+        table = (uint64_t*)r->acc.p;
+      }
+      H.overflow = overflow;
+      for (size_t li = 0; li < nl; ++li)
+        if (r->launches[li].batch == b)
+          if (int rc = launch_one(r, r->launches[li], li, table, H)) return rc;
+      if (r->trim) {
+        const int32_t nb = r->batch_nsegs[b];
+        HIP_OK(hipMemsetAsync(r->t_hist.p, 0, (size_t)r->batch_buckets[b] * 4, st));
+        HIP_OK(hipMemsetAsync(r->t_distinct.p, 0, (size_t)nb * 8, st));
+        HIP_OK(hipMemsetAsync(r->t_bitmap.p, 0, (size_t)nb * 16 * 8, st));
+        const int64_t* bb = (const int64_t*)r->d_bucket_base.p + r->batch_bucket_off[b];
+        HIP_OK(launch_trim(H.keys, H.cap, r->nw + 1, table, r->fd_acc, nb, r->limit, bb, (uint32_t*)r->t_hist.p,
+                           (unsigned long long*)r->t_distinct.p, (int64_t*)r->t_bstar.p, (int64_t*)r->t_rank.p,
+                           (unsigned long long*)r->t_bitmap.p, (int64_t*)r->t_dstar.p, limit_flag, st));
+        HIP_OK(launch_hash_merge(H.keys, H.cap, r->nw, 1, table, (unsigned long long*)r->fkeys.p, r->fcap,
+                                 (uint64_t*)r->acc.p, r->q, r->fd_acc, (const int64_t*)r->t_dstar.p, overflow, st));
+      }
     }
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn, count_grid, 1, 1, pt, 1, 1, (unsigned)r->shmem, st, args, nullptr));
-    HIP_OK(launch_partition_offsets(r->part.hist, r->part.nparts, count_grid, r->part.offs, r->part.part_begin, st));
-    if (r->jit_atomic)
-      HIP_OK(hipModuleLaunchKernel(r->jit_atomic->fn, (unsigned)r->atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn_scatter, (unsigned)r->grid, 1, 1, pt, 1, 1, (unsigned)r->shmem_scatter, st,
-                                 args, nullptr));
-    void* agg_args[] = {(void*)&r->part, (void*)&acc};
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn_agg, (unsigned)r->agg_grid, 1, 1, 1024, 1, 1, (unsigned)r->shmem_agg, st,
-                                 agg_args, nullptr));
-  } else if (r->jit) {
-    const DevSegment* segs = (const DevSegment*)r->d_segs.p;
-    uint64_t* acc = (uint64_t*)r->acc.p;
-    uint64_t* const* bits = r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p;
-    unsigned long long* matched = (unsigned long long*)r->matched.p;
-    void* args[] = {(void*)&segs, (void*)&r->q, (void*)&acc, (void*)&bits, (void*)&matched, (void*)&r->part};
-    HIP_OK(hipModuleLaunchKernel(r->jit->fn, (unsigned)r->grid, 1, 1, kBlock * r->scan_nsub, 1, 1, (unsigned)r->shmem, st, args,
-                                 nullptr));
   } else {
-    HIP_OK(launch_scan((const DevSegment*)r->d_segs.p, r->q, (uint64_t*)r->acc.p,
-                       r->bitsets.empty() ? nullptr : (uint64_t* const*)r->d_bitset_ptrs.p,
-                       (unsigned long long*)r->matched.p, r->grid, st));
+    if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, r->q.num_keys, st));
+    DevHash H{};
+    for (size_t li = 0; li < nl; ++li)
+      if (int rc = launch_one(r, r->launches[li], li, (uint64_t*)r->acc.p, H)) return rc;
   }
   HIP_OK(hipEventRecord(r->ev1, st));
   return 0;
+}
+
+static int64_t next_pow2(int64_t x) {
+  int64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
+static int bits_for(int64_t card) {  // PinotDataBitSet.getNumBitsPerValue(card - 1), at least 1
+  int b = 1;
+  while (b < 62 && ((int64_t)1 << b) < card) ++b;
+  return b;
+}
+static int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+static bool env_is(const char* name, const char* val) {
+  const char* v = getenv(name);
+  return v && strcmp(v, val) == 0;
 }
 
 extern "C" {
@@ -1247,6 +1345,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
                         bool filter_only, pinot_amd_result** out) {
   if (!qq || !segs_in || n < 1 || !out) return fail(PINOT_AMD_EINVAL, "execute: bad arguments");
   std::vector<pinot_amd_segment*> segs(segs_in, segs_in + n);
+  for (auto* s : segs)
+    if (!s) return fail(PINOT_AMD_EINVAL, "execute: null segment");
   auto res = std::make_unique<pinot_amd_result>();
   pinot_amd_result* r = res.get();
   r->stream = (hipStream_t)stream;
@@ -1255,7 +1355,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const pinot_amd_query* Qp = filter_only ? &filter_q : qq;
   pinot_amd_query raw_gb_q;  // group-by columns redirected to the derived dictionary of raw columns
   for (size_t j = 0; j < Qp->group_by.size(); ++j) {
-    const std::string& g = Qp->group_by[j];
+    const std::string g = Qp->group_by[j];  // a copy: the redirect below rewrites Qp->group_by[j]
     int nraw = 0;
     for (auto* s : segs) {
       auto it = s->cols.find(g);
@@ -1290,25 +1390,23 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (!a.column2.empty()) if (int rc = need(a.column2)) return rc;
     }
   }
-  // group-by + aggregation columns always need decoding; predicate columns only if some segment's
-  // leaf reads values (decided below)
-  for (auto& g : Q.group_by) {
-    slot_of(g);
-  }
+  for (auto& g : Q.group_by) slot_of(g);
   for (auto& a : Q.aggs) {
     if (a.column.empty()) continue;
     for (const std::string* col : {&a.column, &a.column2}) {
       if (col->empty()) continue;
-      const Column& c = *segs[0]->cols.at(*col);
-      if (c.type == T_STRING) return fail(PINOT_AMD_EINVAL, "cannot aggregate STRING column %s", col->c_str());
+      for (auto* s : segs)
+        if (s->cols.at(*col)->type != segs[0]->cols.at(*col)->type)
+          return fail(PINOT_AMD_EINVAL, "column %s has different types across segments", col->c_str());
+      if (segs[0]->cols.at(*col)->type == T_STRING) return fail(PINOT_AMD_EINVAL, "cannot aggregate STRING column %s", col->c_str());
       slot_of(*col);
     }
   }
 
-  // ---- per-segment leaves ----
+  // ---- per-segment leaves (PredicateEvaluatorProvider per segment) ----
   const size_t np = Q.preds.size();
   std::vector<std::vector<DevLeaf>> seg_leaves(n, std::vector<DevLeaf>(np));
-  std::vector<std::vector<int>> leaf_slot_col(n, std::vector<int>(np, -1));  // predicate -> slot (or -1)
+  std::vector<std::vector<int>> leaf_slot_col(n, std::vector<int>(np, -1));
   int nclauses = 0;
   for (size_t pi = 0; pi < np; ++pi) nclauses = std::max(nclauses, Q.preds[pi].clause + 1);
   for (int si = 0; si < n; ++si) {
@@ -1324,85 +1422,78 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (needs_slot) leaf_slot_col[si][pi] = slot_of(p.column);
     }
   }
-  if ((int)slot_cols.size() > kMaxSlots) return fail(PINOT_AMD_EUNSUPPORTED, "query reads %zu columns (max %d)",
-                                                    slot_cols.size(), kMaxSlots);
+  if ((int)slot_cols.size() > kMaxSlots)
+    return fail(PINOT_AMD_EUNSUPPORTED, "query reads %zu columns (max %d)", slot_cols.size(), kMaxSlots);
   const int nslots = (int)slot_cols.size();
-
-  // leaf order must be the same for all segments: group by the slot the leaf reads in the
-  // segment where it reads one; a predicate whose leaf is slot-less in some segments keeps its
-  // position and the slot-less segments get a LEAF_CONST/DOC leaf evaluated in that position.
-  // Simplest uniform layout: per predicate choose "slot position" = the slot if any segment needs
-  // it, else slot-less.
+  for (int sl = 0; sl < nslots; ++sl)
+    for (auto* s : segs)
+      if (s->cols.at(slot_cols[sl])->type != segs[0]->cols.at(slot_cols[sl])->type)
+        return fail(PINOT_AMD_EINVAL, "column %s has different types across segments", slot_cols[sl].c_str());
+  // leaf order is the same for all segments: leaves grouped by the slot they read where some segment
+  // reads one, slot-less predicates last (segments where such a leaf resolved slot-less keep its
+  // CONST/DOC kind, which ignores the values)
   std::vector<int> pred_slot(np, -1);
   for (size_t pi = 0; pi < np; ++pi)
     for (int si = 0; si < n; ++si)
       if (leaf_slot_col[si][pi] >= 0) pred_slot[pi] = leaf_slot_col[si][pi];
-  std::vector<size_t> order;  // predicates sorted by slot, slot-less last
+  std::vector<size_t> order;
   for (int sl = 0; sl < nslots; ++sl)
     for (size_t pi = 0; pi < np; ++pi)
       if (pred_slot[pi] == sl) order.push_back(pi);
-  const int slotless_begin = (int)order.size();
   for (size_t pi = 0; pi < np; ++pi)
     if (pred_slot[pi] < 0) order.push_back(pi);
 
   DevQuery& q = r->q;
   memset(&q, 0, sizeof(q));
-  q.nsegs = n;
-  q.nslots = nslots;
-  q.nleaves = (int32_t)np;
-  q.nclauses = nclauses;
-  {
-    int pos = 0;
-    for (int sl = 0; sl < nslots; ++sl) {
-      q.slot_leaf_begin[sl] = pos;
-      for (size_t pi = 0; pi < np; ++pi)
-        if (pred_slot[pi] == sl) ++pos;
-    }
-    for (int sl = nslots; sl <= kMaxSlots; ++sl) q.slot_leaf_begin[sl] = pos;
-    q.slotless_leaf_begin = slotless_begin;
-    q.slotless_leaf_end = (int32_t)np;
-  }
 
-  // ---- group-by key space ----
+  // ---- group-by key space: merged dictionaries (union over the batch, dictionary order) ----
   r->num_group_by = (int32_t)Q.group_by.size();
-  r->num_groups_limit = Q.num_groups_limit;
-  int64_t num_keys = 1;
-  std::vector<std::vector<int32_t>> remaps;  // [g][seg] handled below
+  r->limit = Q.num_groups_limit;
+  double dense_keys = 1;
   for (auto& g : Q.group_by) {
     MergedKeyColumn m;
-    int rc = build_merged_keys(segs, g, &m);
-    if (rc) return rc;
-    r->key_stride.push_back(num_keys);
-    const double nk = (double)num_keys * (double)std::max<size_t>(m.size(), 1);
-    // dense tables stop at 2^28 keys (2 GiB per accumulator array); sparser spaces stay on the Java path
-    if (nk > (double)(1ll << 28)) return fail(PINOT_AMD_EUNSUPPORTED, "group key space %.0f exceeds the dense table", nk);
-    num_keys *= (int64_t)std::max<size_t>(m.size(), 1);
+    if (int rc = build_merged_keys(segs, g, &m)) return rc;
+    r->key_stride.push_back((int64_t)std::min(dense_keys, 9.0e18));
+    dense_keys *= (double)std::max<size_t>(m.size(), 1);
     r->keys.push_back(std::move(m));
   }
-  q.num_keys = num_keys;
+  // numGroupsLimit: a segment can only reach the limit if it can hold that many keys (matching docs
+  // and its own dictionaries' key space bound it); otherwise no trimming can happen
+  std::vector<int64_t> seg_bound(n, 0);
+  bool limit_possible = false;
+  if (!Q.group_by.empty() && !filter_only) {
+    for (int si = 0; si < n; ++si) {
+      double b = (double)segs[si]->num_docs;
+      double ks = 1;
+      for (auto& g : Q.group_by) ks *= (double)std::max(segs[si]->cols.at(g)->card, 1);
+      b = std::min(b, ks);
+      seg_bound[si] = (int64_t)b;
+      limit_possible |= seg_bound[si] >= Q.num_groups_limit;
+    }
+  }
+  r->limit_possible = limit_possible;
 
-  // ---- accumulators: acc 0 = COUNT; others grouped by slot ----
+  // ---- accumulators: acc 0 = COUNT; others grouped by slot; ACC_FIRST_DOC last ----
   struct AccReq { int slot; int op; int expr; int slot2; };
   std::vector<AccReq> reqs;
   std::vector<int> agg_req(Q.aggs.size(), -1);
-  bool any_expr = false;
   for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
     const AggSpec& a = Q.aggs[ai];
     if (a.type == PINOT_AMD_AGG_COUNT) continue;
     const Column& c = *segs[0]->cols.at(a.column);
-    // an expression sums exactly in int64 when both operands are INT (every partial sum of the
-    // reference's double accumulation is then exact below 2^53), otherwise in double
+    // SUM / AVG of integer values are summed exactly in 128 bits (SumAggregationFunction accumulates
+    // in double: equal whenever partial sums stay below 2^53, and the correctly rounded exact sum
+    // beyond); an expression is integer when both operands are INT (the product fits 64 bits)
     const bool expr_int = a.expr != PINOT_AMD_EXPR_COLUMN && c.type == T_INT &&
                           segs[0]->cols.at(a.column2)->type == T_INT;
-    any_expr |= a.expr != PINOT_AMD_EXPR_COLUMN;
     int op;
     switch (a.type) {
       case PINOT_AMD_AGG_SUM:
       case PINOT_AMD_AGG_AVG:
-        if (a.expr != PINOT_AMD_EXPR_COLUMN) op = expr_int ? ACC_SUM_I64 : ACC_SUM_F64;
-        else op = is_float(c.type) ? ACC_SUM_F64 : ACC_SUM_I64;
+        if (a.expr != PINOT_AMD_EXPR_COLUMN) op = expr_int ? ACC_SUM_I128 : ACC_SUM_F64;
+        else op = is_float(c.type) ? ACC_SUM_F64 : ACC_SUM_I128;
         break;
-      case PINOT_AMD_AGG_SUMLONG:
+      case PINOT_AMD_AGG_SUMLONG:  // Java long arithmetic: wraps
         if (is_float(c.type)) return fail(PINOT_AMD_EINVAL, "SUMLONG on floating column %s", a.column.c_str());
         op = ACC_SUM_I64;
         break;
@@ -1420,42 +1511,118 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     agg_req[ai] = found;
   }
-  if ((int)reqs.size() + 1 > kMaxAcc) return fail(PINOT_AMD_EUNSUPPORTED, "too many aggregations");
   std::vector<int> req_acc(reqs.size());
-  std::vector<AccReq> acc_req(kMaxAcc, AccReq{0, 0, 0, -1});  // accumulator index -> its request
-  q.nacc = 1;
+  std::vector<AccReq> acc_req(kMaxAcc + 2, AccReq{0, 0, 0, -1});
+  int nacc = 1;
   q.acc_op[0] = ACC_COUNT;
-  for (int sl = 0; sl < kMaxSlots; ++sl) {
-    q.slot_acc_begin[sl] = q.nacc;
+  auto push_acc = [&](const AccReq& rq) -> int {
+    if (nacc >= kMaxAcc) return fail(PINOT_AMD_EUNSUPPORTED, "too many aggregations");
+    acc_req[nacc] = rq;
+    q.acc_op[nacc++] = rq.op;
+    return 0;
+  };
+  for (int sl = 0; sl < kMaxSlots; ++sl)
     for (size_t k = 0; k < reqs.size(); ++k)
       if (reqs[k].slot == sl) {
-        req_acc[k] = q.nacc;
-        acc_req[q.nacc] = reqs[k];
-        q.acc_op[q.nacc++] = reqs[k].op;
+        req_acc[k] = nacc;
+        if (int rc = push_acc(reqs[k])) return rc;
+        if (reqs[k].op == ACC_SUM_I128)
+          if (int rc = push_acc({reqs[k].slot, ACC_HI, reqs[k].expr, reqs[k].slot2})) return rc;
       }
-  }
-  q.slot_acc_begin[kMaxSlots] = q.nacc;
   for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
     r->agg_type.push_back(Q.aggs[ai].type);
     r->agg_acc.push_back(agg_req[ai] < 0 ? 0 : req_acc[agg_req[ai]]);
   }
-  for (size_t j = 0; j < Q.group_by.size(); ++j) q.slot_group_stride[slot_of(Q.group_by[j])] = r->key_stride[j];
-  if (Q.aggs.empty() && Q.group_by.empty()) q.nacc = 0;  // filter-only: count matches
-  q.agg_only = Q.group_by.empty() ? 1 : 0;
 
-  // LDS-privatised table when it fits in 40 KB (keeps >= 4 blocks of 256 threads per CU)
-  const int64_t lds_bytes = (int64_t)q.nacc * num_keys * 8;
-  q.lds_keys = (q.nacc > 0 && lds_bytes <= 40 * 1024) ? (int32_t)num_keys : 0;
+  // ---- plan kind ----
+  // dense table: mixed-radix keys over the merged dictionaries; hash table: key spaces beyond the
+  // dense cap (DictionaryBasedGroupKeyGenerator's Int/Long/ArrayMapBasedHolder) and numGroupsLimit
+  // trimming (keys admitted per segment in first-seen order)
+  const int64_t dense_cap = env_i64("PINOT_AMD_DENSE_MAX_KEYS", (int64_t)1 << 28);
+  if (filter_only) {
+    r->kind = PLAN_FILTER;
+  } else if (Q.group_by.empty()) {
+    r->kind = PLAN_DENSE;
+  } else if (limit_possible || dense_keys > (double)dense_cap || env_is("PINOT_AMD_GROUP_PLAN", "hash")) {
+    r->kind = PLAN_HASH;
+    r->trim = limit_possible;
+  } else {
+    r->kind = PLAN_DENSE;
+  }
+  if (r->trim) {
+    r->fd_acc = nacc;
+    if (int rc = push_acc({-1, ACC_FIRST_DOC, 0, -1})) return rc;
+  }
+  q.nacc = (Q.aggs.empty() && Q.group_by.empty()) ? 0 : nacc;  // filter-only: count matches
+  if (filter_only) q.nacc = 0;
+  const int64_t num_keys = r->kind == PLAN_HASH ? 0 : (int64_t)dense_keys;
+  q.num_keys = num_keys;
 
-  // ---- device segments ----
-  r->hsegs.resize(n);
-  int64_t tiles = 0;
+  // ---- hash plans: key packing and table sizes ----
+  const int64_t table_budget = env_i64("PINOT_AMD_HASH_TABLE_BYTES", (int64_t)4 << 30);  // per trim scan table
+  std::vector<int> seg_batch(n, 0);
+  if (r->kind == PLAN_HASH) {
+    int w = 0, sh = 0;
+    for (auto& m : r->keys) {
+      const int b = bits_for((int64_t)std::max<size_t>(m.size(), 1));
+      if (sh + b > 63) { ++w; sh = 0; }
+      r->pack_word.push_back(w);
+      r->pack_shift.push_back(sh);
+      r->pack_bits.push_back(b);
+      sh += b;
+    }
+    r->nw = w + 1;
+    if (r->nw + (r->trim ? 1 : 0) > kMaxKeyWords)
+      return fail(PINOT_AMD_EUNSUPPORTED, "group key of %d words exceeds %d", r->nw, kMaxKeyWords);
+    const double keyspace = dense_keys;
+    double fbound = 0;
+    for (int si = 0; si < n; ++si) fbound += (double)(r->trim ? std::min<int64_t>(seg_bound[si], Q.num_groups_limit) : seg_bound[si]);
+    fbound = std::min(fbound, keyspace);
+    const int64_t max_cap = (int64_t)1 << 31;  // compaction indexes slots with int32
+    auto bytes_of = [&](int64_t cap, int words) { return (double)cap * (double)(words + nacc) * 8.0; };
+    // the final table holds every admitted group at once (it cannot be batched)
+    const int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)std::min(2.0 * fbound, (double)max_cap)));
+    const double fbytes = bytes_of(fcap, r->nw);
+    if (fbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
+      return fail(PINOT_AMD_EUNSUPPORTED, "group table of %lld slots (%.1f GB) exceeds PINOT_AMD_HASH_FINAL_MAX_BYTES",
+                  (long long)fcap, fbytes / 1e9);
+    r->fcap = fcap;
+    if (r->trim) {
+      // scan tables keyed by (key, segment), one batch of segments at a time
+      int b = 0;
+      double acc_bound = 0;
+      int bsegs = 0;
+      auto close_batch = [&]() {
+        const int64_t cap = next_pow2(std::max<int64_t>(64, (int64_t)std::min(2.0 * acc_bound, (double)max_cap)));
+        r->batch_cap.push_back(cap);
+        r->batch_nsegs.push_back(bsegs);
+      };
+      for (int si = 0; si < n; ++si) {
+        const double nb = acc_bound + (double)seg_bound[si];
+        const int64_t cap = next_pow2(std::max<int64_t>(64, (int64_t)std::min(2.0 * nb, (double)max_cap)));
+        if (bsegs > 0 && (bytes_of(cap, r->nw + 1) > (double)table_budget || 2.0 * nb > (double)max_cap)) {
+          close_batch();
+          ++b;
+          acc_bound = 0;
+          bsegs = 0;
+        }
+        seg_batch[si] = b;
+        acc_bound += (double)seg_bound[si];
+        ++bsegs;
+      }
+      close_batch();
+      r->nbatches = b + 1;
+      for (int64_t c : r->batch_cap)
+        if ((double)c < 2.0 * 1) return fail(PINOT_AMD_EINVAL, "internal: empty trim batch");
+    }
+  }
+
+  // ---- device segments (one DevSegment per segment; tile_begin / key_seg set per launch) ----
+  std::vector<DevSegment> hsegs(n);
   for (int si = 0; si < n; ++si) {
-    DevSegment& ds = r->hsegs[si];
+    DevSegment& ds = hsegs[si];
     memset(&ds, 0, sizeof(ds));
     ds.num_docs = segs[si]->num_docs;
-    ds.tile_begin = tiles;
-    tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
     for (int sl = 0; sl < nslots; ++sl) {
       const Column& c = *segs[si]->cols.at(slot_cols[sl]);
       DevColumn& dc = ds.cols[sl];
@@ -1474,25 +1641,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       for (size_t d = 0; identity && d < rm.size(); ++d) identity = rm[d] == (int32_t)d;
       if (!identity) {
         auto buf = std::make_unique<DevBuf>();
-        int rc = buf->alloc_copy(rm.data(), rm.size() * 4, 64);
-        if (rc) return rc;
+        if (int rc = buf->alloc_copy(rm.data(), rm.size() * 4, 64)) return rc;
         ds.cols[slot_of(Q.group_by[j])].remap = (const int32_t*)buf->p;
         r->owned.push_back(std::move(buf));
       }
     }
     for (size_t k = 0; k < order.size(); ++k) {
       DevLeaf L = seg_leaves[si][order[k]];
-      // leaves that resolved slot-less in this segment but sit in a slot group keep kind
-      // (CONST/DOC_*), which ignore the values
       L.slot = pred_slot[order[k]];
       ds.leaves[k] = L;
     }
   }
-  q.total_tiles = tiles;
-  if (tiles == 0) q.total_tiles = 0;
-
-  int rc = r->d_segs.alloc_copy(r->hsegs.data(), r->hsegs.size() * sizeof(DevSegment), 0);
-  if (rc) return rc;
   if (!r->inv_leaves.empty()) {
     std::vector<ExpandJob> jobs(r->inv_leaves.size());
     int64_t total = 0, items = 0;
@@ -1515,149 +1674,202 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       items += il.nchunks;
     }
     r->expand_total = items;
-    rc = r->d_expand_jobs.alloc_copy(jobs.data(), jobs.size() * sizeof(ExpandJob), 0);
-    if (rc) return rc;
+    if (int rc = r->d_expand_jobs.alloc_copy(jobs.data(), jobs.size() * sizeof(ExpandJob), 0)) return rc;
   }
+  std::vector<uint64_t*> bitset_ptrs(n, nullptr);
   if (filter_only) {
-    std::vector<uint64_t*> ptrs;
     for (int si = 0; si < n; ++si) {
       const int64_t words = std::max<int64_t>((segs[si]->num_docs + kTileDocs - 1) / kTileDocs, 1) * (kTileDocs / 64);
       auto b = std::make_unique<DevBuf>();
-      rc = b->alloc((size_t)words * 8);
-      if (rc) return rc;
+      if (int rc = b->alloc((size_t)words * 8)) return rc;
       HIP_OK(hipMemset(b->p, 0, b->n));
-      ptrs.push_back((uint64_t*)b->p);
+      bitset_ptrs[si] = (uint64_t*)b->p;
       r->bitset_words.push_back(words);
       r->bitsets.push_back(std::move(b));
     }
-    rc = r->d_bitset_ptrs.alloc_copy(ptrs.data(), ptrs.size() * sizeof(uint64_t*), 0);
-    if (rc) return rc;
   }
-  rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * num_keys * 8);
-  if (rc) return rc;
-  rc = r->matched.alloc(3 * sizeof(unsigned long long));
-  if (rc) return rc;
 
-  // query-specialised kernel (hipRTC): needs every slot's encoding to agree across the batch
-  bool jp_lds = false;
-  int jp_scan_nsub = 1;
+  // ---- plan-level kernel choices (shared by every launch) ----
+  int lds_max = 0;
   {
-    JitPlan jp;
-    bool ok = true;
-    for (int sl = 0; sl < nslots && ok; ++sl) {
-      const int enc = r->hsegs[0].cols[sl].enc;
-      for (int si = 1; si < n; ++si) ok &= r->hsegs[si].cols[sl].enc == enc;
-      JitSlot js{enc, r->hsegs[0].cols[sl].type, 0, 0};
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) lds_max = 65536;
+    lds_max = std::min(lds_max, 160 * 1024);
+  }
+  JitPlan base;
+  base.nclauses = nclauses;
+  for (size_t j = 0; j < Q.group_by.size(); ++j) {
+    base.group.push_back({slot_of(Q.group_by[j]), r->kind == PLAN_HASH ? 0 : r->key_stride[j]});
+    for (int si = 0; si < n; ++si) base.any_remap |= hsegs[si].cols[slot_of(Q.group_by[j])].remap != nullptr;
+  }
+  for (int a = 1; a < q.nacc; ++a) base.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2});
+  base.num_keys = num_keys;
+  base.bitset = filter_only;
+  base.aggregate = q.nacc > 0;
+  const int64_t lds_bytes = (int64_t)q.nacc * std::max<int64_t>(num_keys, 1) * 8;
+  if (r->kind == PLAN_DENSE && q.nacc > 0) {
+    if (lds_bytes <= 40 * 1024) {  // LDS-privatised table, four 256-thread blocks per CU
+      base.lds = true;
+    } else if (lds_bytes <= lds_max && !env_is("PINOT_AMD_WIDE_LDS", "0")) {
+      base.lds = true;  // one CU-wide block (4 x 256 threads, 16 waves) owns the whole table
+      base.scan_nsub = kPartSub;
+    } else if (!env_is("PINOT_AMD_PARTITIONED", "0") && !Q.group_by.empty()) {
+      // key space too large for an LDS table: partition the matching docs by key range and aggregate
+      // each partition in LDS (random per-lane HBM atomics run ~17x below the coalesced rate)
+      int shift = 16;
+      while (shift > 6 && (int64_t)q.nacc * ((int64_t)1 << shift) * 8 > lds_max) --shift;
+      const int64_t nparts = (num_keys + ((int64_t)1 << shift) - 1) >> shift;
+      if ((int64_t)q.nacc * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
+        r->kind = PLAN_PARTITIONED;
+        base.partitioned = true;
+        base.key_shift = shift;
+        base.nparts = (int)nparts;
+        for (auto& a : base.accs)
+          if (a.op != ACC_HI && a.op != ACC_FIRST_DOC &&
+              std::find(base.vals.begin(), base.vals.end(), a.val()) == base.vals.end())
+            base.vals.push_back(a.val());
+      }
+    }
+  }
+  if (r->kind == PLAN_HASH) {
+    base.hash = true;
+    base.hash_seg = r->trim;
+    base.hash_words = r->nw + (r->trim ? 1 : 0);
+    for (size_t j = 0; j < Q.group_by.size(); ++j) base.hash_pack.push_back({r->pack_word[j], r->pack_shift[j]});
+  }
+
+  // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
+  int dev = 0, cus = 256;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
+  std::vector<int32_t> key_seg(n, 0);
+  {
+    std::vector<int32_t> cnt(r->nbatches, 0);
+    for (int si = 0; si < n; ++si) key_seg[si] = cnt[seg_batch[si]]++;
+  }
+  for (int b = 0; b < r->nbatches; ++b) {
+    // encoding signature -> segments; within it, fixed-bit width signatures
+    std::map<std::string, std::vector<int>> by_enc;
+    std::vector<std::string> enc_order;
+    for (int si = 0; si < n; ++si) {
+      if (seg_batch[si] != b) continue;
+      std::string sig;
+      for (int sl = 0; sl < nslots; ++sl) sig += std::to_string(hsegs[si].cols[sl].enc) + ",";
+      if (!by_enc.count(sig)) enc_order.push_back(sig);
+      by_enc[sig].push_back(si);
+    }
+    for (const std::string& es : enc_order) {
+      const std::vector<int>& group = by_enc[es];
+      auto bits_sig = [&](int si) {
+        std::string sig;
+        for (int sl = 0; sl < nslots; ++sl)
+          sig += std::to_string(hsegs[si].cols[sl].enc == ENC_FIXED_BIT && hsegs[si].cols[sl].bits <= 15 ? hsegs[si].cols[sl].bits : 0) + ",";
+        return sig;
+      };
+      std::map<std::string, std::vector<int>> by_bits;
+      std::vector<std::string> bits_order;
+      for (int si : group) {
+        const std::string sig = bits_sig(si);
+        if (!by_bits.count(sig)) bits_order.push_back(sig);
+        by_bits[sig].push_back(si);
+      }
+      std::vector<std::vector<int>> parts;
+      if (bits_order.size() <= 3) {
+        for (auto& sig : bits_order) parts.push_back(by_bits[sig]);
+      } else {
+        parts.push_back(group);  // many widths: one launch with run-time widths where they differ
+      }
+      for (auto& part_segs : parts) {
+        r->launches.emplace_back();
+        Launch& L = r->launches.back();
+        L.segs = part_segs;
+        L.batch = b;
+      }
+    }
+  }
+  const size_t nl = r->launches.size();
+  if (int rc = r->matched.alloc((3 * nl + 2) * sizeof(unsigned long long))) return rc;
+  HIP_OK(hipMemset(r->matched.p, 0, r->matched.n));
+  size_t max_count_cells = 0, max_rec = 0;
+  for (size_t li = 0; li < nl; ++li) {
+    Launch& L = r->launches[li];
+    std::vector<DevSegment> ls;
+    std::vector<uint64_t*> lbits;
+    int64_t tiles = 0;
+    for (int si : L.segs) {
+      DevSegment ds = hsegs[si];
+      ds.tile_begin = tiles;
+      ds.key_seg = key_seg[si];
+      tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
+      L.docs += segs[si]->num_docs;
+      ls.push_back(ds);
+      lbits.push_back(bitset_ptrs[si]);
+    }
+    L.tiles = tiles;
+    L.q = q;
+    L.q.nsegs = (int32_t)L.segs.size();
+    L.q.total_tiles = tiles;
+    if (int rc = L.d_segs.alloc_copy(ls.data(), ls.size() * sizeof(DevSegment), 0)) return rc;
+    if (filter_only)
+      if (int rc = L.d_bitset_ptrs.alloc_copy(lbits.data(), lbits.size() * sizeof(uint64_t*), 0)) return rc;
+
+    JitPlan jp = base;
+    for (int sl = 0; sl < nslots; ++sl) {
+      const int enc = ls[0].cols[sl].enc;
+      JitSlot js{enc, ls[0].cols[sl].type, 0, 0};
       if (enc != ENC_RAW) {  // dictionary of <= 64 entries everywhere: lane-register table
         bool small = true;
-        for (int si = 0; si < n; ++si) small &= r->hsegs[si].cols[sl].card <= 64 && r->hsegs[si].cols[sl].card > 0;
+        for (auto& d : ls) small &= d.cols[sl].card <= 64 && d.cols[sl].card > 0;
         js.dict_regs = small ? 1 : 0;
       }
-      if (enc == ENC_FIXED_BIT) {
-        // bit width shared by the whole batch (and <= 15): decode with compile-time shifts
-        js.bits = r->hsegs[0].cols[sl].bits;
-        for (int si = 1; si < n; ++si)
-          if (r->hsegs[si].cols[sl].bits != js.bits || r->hsegs[si].cols[sl].enc != enc) js.bits = 0;
-        if (js.bits > 15) js.bits = 0;
-        if (const char* gb = getenv("PINOT_AMD_GENERIC_BITS"))
-          if (strcmp(gb, "1") == 0) js.bits = 0;
+      if (enc == ENC_FIXED_BIT) {  // width shared by the launch (<= 15): compile-time shifts
+        js.bits = ls[0].cols[sl].bits;
+        for (auto& d : ls)
+          if (d.cols[sl].bits != js.bits) js.bits = 0;
+        if (js.bits > 15 || generic_bits) js.bits = 0;
       }
       jp.slots.push_back(js);
     }
     for (size_t k = 0; k < order.size(); ++k) {
-      JitLeaf jl{pred_slot[order[k]], Q.preds[order[k]].clause, r->hsegs[0].leaves[k].negate, 0u};
+      JitLeaf jl{pred_slot[order[k]], Q.preds[order[k]].clause, ls[0].leaves[k].negate, 0u};
       bool small_sets = jl.slot >= 0;
-      for (int si = 0; si < n; ++si) {
-        ok &= r->hsegs[si].leaves[k].negate == jl.negate;
-        jl.kinds |= 1u << r->hsegs[si].leaves[k].kind;
-        if (jl.slot >= 0) small_sets &= r->hsegs[si].cols[jl.slot].card < 64 * 32;
+      for (auto& d : ls) {
+        jl.kinds |= 1u << d.leaves[k].kind;
+        if (jl.slot >= 0) small_sets &= d.cols[jl.slot].card < 64 * 32;
       }
-      // dictId-set bitmask of <= 64 words in every segment: one word per lane
       jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
       jp.leaves.push_back(jl);
     }
-    jp.nclauses = nclauses;
-    for (size_t j = 0; j < Q.group_by.size(); ++j) {
-      const int sl = slot_of(Q.group_by[j]);
-      jp.group.push_back({sl, r->key_stride[j]});
-      for (int si = 0; si < n; ++si) jp.any_remap |= r->hsegs[si].cols[sl].remap != nullptr;
-    }
-    for (int a = 1; a < q.nacc; ++a)
-      jp.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2});
-    jp.num_keys = num_keys;
-    // pipeline depth from the bytes a wave has in flight per tile (256 docs x bytes per row):
-    // aim for ~4 KiB per wave (~64-96 KiB per CU at 16-24 resident waves) to cover HBM latency
-    {
+    {  // pipeline depth: ~4 KiB in flight per wave (256 docs x bytes per row)
       double bpr = 0;
       for (const JitSlot& js : jp.slots)
         bpr += js.enc == ENC_FIXED_BIT ? (js.bits > 0 ? js.bits : 16) / 8.0 : js.enc == ENC_RAW ? value_size(js.type) : 0.0;
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
       if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
-      if (const char* lr = getenv("PINOT_AMD_LANE_TABLES"))
-        if (strcmp(lr, "0") == 0) {
-          for (auto& js : jp.slots) js.dict_regs = 0;
-          for (auto& jl : jp.leaves) jl.bits_regs = 0;
-        }
+      if (env_is("PINOT_AMD_LANE_TABLES", "0")) {
+        for (auto& js : jp.slots) js.dict_regs = 0;
+        for (auto& jl : jp.leaves) jl.bits_regs = 0;
+      }
       if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
     }
-    jp.lds = q.lds_keys > 0;
-    jp.bitset = filter_only;
-    jp.aggregate = q.nacc > 0;
-    int lds_max = 0;
-    {
-      int dev = 0;
-      HIP_OK(hipGetDevice(&dev));
-      if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) lds_max = 65536;
-      lds_max = std::min(lds_max, 160 * 1024);
+    if (jp.partitioned) {
+      jit_layout_records(&jp);
+      // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a run is
+      // too short to pay for the staging round trip and records are written directly
+      int cap = 64;
+      while (cap >= 4 && jit_scatter_lds(jp, cap) > (size_t)lds_max) --cap;
+      jp.stage_cap = cap >= 4 ? cap : 0;
+      if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
     }
-    // group table above the 40 KiB that keeps four 256-thread blocks per CU but within one
-    // workgroup's LDS: one CU-wide block (4 x 256 threads, 16 waves) owns the whole table
-    if (!jp.lds && q.nacc > 0 && !filter_only && lds_bytes <= lds_max) {
-      const char* wl = getenv("PINOT_AMD_WIDE_LDS");
-      if (!(wl && strcmp(wl, "0") == 0)) {
-        jp.lds = true;
-        jp.scan_nsub = kPartSub;
-      }
-    }
-    // key space too large for an LDS table: partition the matching docs by key range and
-    // aggregate each partition in LDS (per-lane HBM atomics on random keys run ~17x below the
-    // coalesced atomic rate). Keys per partition: the largest power of two whose nacc tables fit
-    // in one workgroup's LDS (gfx950: 160 KiB); local keys are 16-bit.
-    const char* pe = getenv("PINOT_AMD_PARTITIONED");
-    const bool allow_part = !(pe && strcmp(pe, "0") == 0);
-    if (ok && allow_part && !filter_only && q.nacc > 0 && !jp.lds && !Q.group_by.empty()) {
-      int shift = 16;
-      while (shift > 6 && (int64_t)q.nacc * ((int64_t)1 << shift) * 8 > lds_max) --shift;
-      const int64_t nparts = (num_keys + ((int64_t)1 << shift) - 1) >> shift;
-      if ((int64_t)q.nacc * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
-        jp.partitioned = true;
-        jp.key_shift = shift;
-        jp.nparts = (int)nparts;
-        for (auto& a : jp.accs)
-          if (std::find(jp.vals.begin(), jp.vals.end(), a.val()) == jp.vals.end()) jp.vals.push_back(a.val());
-        jit_layout_records(&jp);
-        // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a
-        // run is too short to pay for the staging round trip and records are written directly
-        int cap = 64;
-        while (cap >= 4 && jit_scatter_lds(jp, cap) > (size_t)lds_max) --cap;
-        jp.stage_cap = cap >= 4 ? cap : 0;
-        if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
-      }
-    }
-    if (ok) {
-      r->jit = jit_get(jp, &r->jit_status);
-    } else {
-      r->jit_status = "segments disagree on a column's encoding";
-    }
-    jp_lds = jp.lds && !jp.partitioned;
-    jp_scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
-    if (!r->jit && any_expr)  // the generic AOT kernel reads plain columns only: fail loudly
-      return fail(PINOT_AMD_EUNSUPPORTED, "aggregation over an expression needs the query-specialised kernel (%s)",
-                  r->jit_status.c_str());
-    if (r->jit && jp.partitioned) {
-      // companion direct-atomic scan for batches where the filter keeps few docs (decided on the
-      // device from the count pass): atomics on so few keys cost less than writing records
-      JitPlan ja = jp;
+    L.jit = jit_get(jp, &r->jit_status);
+    if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
+    L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
+    L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : 0;
+    int per_cu = 1;
+    if (jp.partitioned) {
+      JitPlan ja = jp;  // companion direct-atomic scan for batches where the filter keeps few docs
       ja.partitioned = false;
       ja.lds = false;
       ja.scan_nsub = 1;
@@ -1665,108 +1877,119 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       ja.vals.clear();
       ja.val_off.clear();
       ja.rec_bytes = ja.stage_cap = ja.nparts = ja.key_shift = 0;
-      const char* ag = getenv("PINOT_AMD_ATOMIC_HANDOVER");
-      if (!(ag && strcmp(ag, "0") == 0)) {
+      if (!env_is("PINOT_AMD_ATOMIC_HANDOVER", "0")) {
         std::string err;
-        r->jit_atomic = jit_get(ja, &err);
+        L.jit_atomic = jit_get(ja, &err);
       }
-      int64_t docs = 0;
-      for (auto* s : segs) docs += s->num_docs;
-      r->part.atomic_threshold = r->jit_atomic ? docs / 64 : -1;
-      if (ag && strcmp(ag, "force") == 0 && r->jit_atomic) r->part.atomic_threshold = INT64_MAX;
-      // selectivity sample: the filter over every 32nd tile (~3% of the filter columns' bytes); when
-      // the extrapolated matches fall under the threshold the count pass steps aside and the
-      // direct-atomic scan is the only full pass (a misestimate costs time, never correctness)
-      const char* sp = getenv("PINOT_AMD_SAMPLE_STRIDE");
-      const int64_t stride = sp ? atoll(sp) : 32;
-      if (r->jit_atomic && stride > 0 && tiles >= 64 * stride) {
+      L.part.atomic_threshold = L.jit_atomic ? L.docs / 64 : -1;
+      if (env_is("PINOT_AMD_ATOMIC_HANDOVER", "force") && L.jit_atomic) L.part.atomic_threshold = INT64_MAX;
+      // selectivity sample over every 32nd tile: when the extrapolated matches fall under the threshold
+      // the count pass steps aside and the direct-atomic scan is the only full pass
+      const int64_t stride = env_i64("PINOT_AMD_SAMPLE_STRIDE", 32);
+      if (L.jit_atomic && stride > 0 && tiles >= 64 * stride) {
         JitPlan js = ja;
         js.atomic_gate = false;
         js.sample = true;
         js.aggregate = false;
         std::string err;
-        r->jit_sample = jit_get(js, &err);
-        if (r->jit_sample) r->part.sample_stride = stride;
+        L.jit_sample = jit_get(js, &err);
+        if (L.jit_sample) L.part.sample_stride = stride;
       }
-      r->partitioned = true;
-      r->part.nparts = jp.nparts;
-      r->part.key_shift = jp.key_shift;
-      r->shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
-      r->shmem_agg = (size_t)q.nacc * ((size_t)1 << jp.key_shift) * 8;
-      int64_t total_docs = 0;
-      for (auto* s : segs) total_docs += s->num_docs;
-      rc = r->rec.alloc((size_t)total_docs * jp.rec_bytes + 256);
-      if (rc) return rc;
-      r->part.rec = (uint8_t*)r->rec.p;
-      r->rec_bytes = jp.rec_bytes;
-      r->stage_cap = jp.stage_cap;
+      L.part.nparts = jp.nparts;
+      L.part.key_shift = jp.key_shift;
+      L.shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
+      L.shmem_agg = (size_t)q.nacc * ((size_t)1 << jp.key_shift) * 8;
+      L.shmem = (size_t)jp.nparts * 4;
+      max_rec = std::max(max_rec, (size_t)L.docs * jp.rec_bytes + 256);
+      int nb = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn_scatter, kBlock * kPartSub, L.shmem_scatter) !=
+              hipSuccess || nb < 1)
+        nb = 1;
+      per_cu = nb;
+      int na = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&na, L.jit->fn_agg, 1024, L.shmem_agg) != hipSuccess || na < 1)
+        na = 1;
+      L.agg_grid = cus * na;
+      if (L.jit_atomic) {
+        int nt = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nt, L.jit_atomic->fn, kBlock, 0) != hipSuccess || nt < 1) nt = 1;
+        L.atomic_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nt, tiles));
+      }
+      if (L.jit_sample) {
+        int ns = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, L.jit_sample->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
+        const int64_t vt = (tiles + L.part.sample_stride - 1) / L.part.sample_stride;
+        L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
+      }
+      L.part.counts = (unsigned long long*)r->matched.p + 3 * li;
+    } else {
+      int nb = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||
+          nb < 1)
+        nb = 1;
+      per_cu = nb;
+    }
+    // persistent grid: resident blocks per CU x CUs (a larger grid would only queue a tail)
+    int64_t grid = (int64_t)cus * per_cu;
+    if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
+    if ((jp.partitioned || L.scan_nsub > 1) && grid * kPartSub > tiles) grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
+    L.grid = (int)grid;
+    if (jp.partitioned) max_count_cells = std::max(max_count_cells, (size_t)jp.nparts * (size_t)grid * kPartCountRatio);
+  }
+  // partitioned work buffers, shared by the launches (they run one after another)
+  if (r->kind == PLAN_PARTITIONED) {
+    int maxp = 0;
+    for (auto& L : r->launches) maxp = std::max(maxp, L.part.nparts);
+    if (int rc = r->hist.alloc(max_count_cells * 4)) return rc;
+    if (int rc = r->offs.alloc(max_count_cells * 8)) return rc;
+    if (int rc = r->part_begin.alloc(((size_t)maxp + 1) * 8)) return rc;
+    if (int rc = r->rec.alloc(max_rec)) return rc;
+    for (auto& L : r->launches) {
+      L.part.hist = (uint32_t*)r->hist.p;
+      L.part.offs = (int64_t*)r->offs.p;
+      L.part.part_begin = (int64_t*)r->part_begin.p;
+      L.part.rec = (uint8_t*)r->rec.p;
     }
   }
-  r->scan_nsub = r->jit ? jp_scan_nsub : 1;
-  r->shmem = (q.lds_keys > 0 || (r->jit && jp_lds)) ? (size_t)lds_bytes : 0;
-  if (r->partitioned) r->shmem = (size_t)r->part.nparts * 4;
-
-  // persistent grid: enough blocks to fill every CU at the occupancy the LDS table allows
-  int dev = 0, cus = 256;
-  HIP_OK(hipGetDevice(&dev));
-  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  // resident blocks per CU (VGPR / LDS limited): a larger grid would only queue a second, tail-heavy wave
-  int per_cu = 1;
-  if (r->jit && r->partitioned) {
-    // count and scatter passes must share the block -> tile mapping: size for the scatter pass
-    int nb = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn_scatter, kBlock * kPartSub,
-                                                           r->shmem_scatter) != hipSuccess || nb < 1)
-      nb = 1;
-    per_cu = nb;
-    int na = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&na, r->jit->fn_agg, 1024, r->shmem_agg) != hipSuccess ||
-        na < 1)
-      na = 1;
-    r->agg_grid = cus * na;
-    if (r->jit_atomic) {
-      int nt = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nt, r->jit_atomic->fn, kBlock, 0) != hipSuccess || nt < 1)
-        nt = 1;
-      r->atomic_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nt, tiles));
+  // accumulator tables
+  if (r->kind == PLAN_HASH) {
+    if (int rc = r->fkeys.alloc((size_t)r->nw * (size_t)r->fcap * 8)) return rc;
+    if (int rc = r->acc.alloc((size_t)q.nacc * (size_t)r->fcap * 8)) return rc;
+    if (r->trim) {
+      const int64_t scap = *std::max_element(r->batch_cap.begin(), r->batch_cap.end());
+      if (int rc = r->skeys.alloc((size_t)(r->nw + 1) * (size_t)scap * 8)) return rc;
+      if (int rc = r->sacc.alloc((size_t)q.nacc * (size_t)scap * 8)) return rc;
+      // per batch: bucket_base (1024-doc buckets of first docIds per segment)
+      std::vector<int64_t> bb;
+      int32_t maxnb = 0;
+      int64_t maxbk = 0;
+      for (int b = 0; b < r->nbatches; ++b) {
+        r->batch_bucket_off.push_back((int64_t)bb.size());
+        int64_t acc_b = 0;
+        for (int si = 0; si < n; ++si) {
+          if (seg_batch[si] != b) continue;
+          bb.push_back(acc_b);
+          acc_b += (segs[si]->num_docs + 1023) / 1024;
+        }
+        bb.push_back(acc_b);
+        r->batch_buckets.push_back(acc_b);
+        maxnb = std::max(maxnb, r->batch_nsegs[b]);
+        maxbk = std::max(maxbk, acc_b);
+      }
+      if (int rc = r->d_bucket_base.alloc_copy(bb.data(), bb.size() * 8, 0)) return rc;
+      if (int rc = r->t_hist.alloc((size_t)std::max<int64_t>(maxbk, 1) * 4)) return rc;
+      if (int rc = r->t_distinct.alloc((size_t)maxnb * 8)) return rc;
+      if (int rc = r->t_bstar.alloc((size_t)maxnb * 8)) return rc;
+      if (int rc = r->t_rank.alloc((size_t)maxnb * 8)) return rc;
+      if (int rc = r->t_dstar.alloc((size_t)maxnb * 8)) return rc;
+      if (int rc = r->t_bitmap.alloc((size_t)maxnb * 16 * 8)) return rc;
     }
-    if (r->jit_sample) {
-      int ns = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, r->jit_sample->fn, kBlock, 0) != hipSuccess || ns < 1)
-        ns = 1;
-      const int64_t vt = (tiles + r->part.sample_stride - 1) / r->part.sample_stride;
-      // a few tiles per wave: the sample is latency-bound, not bandwidth-bound
-      r->sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
-    }
-    r->part.counts = (unsigned long long*)r->matched.p;
-  } else if (r->jit) {
-    int nb = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r->jit->fn, kBlock * r->scan_nsub, r->shmem) !=
-            hipSuccess || nb < 1)
-      nb = 1;
-    per_cu = nb;
   } else {
-    per_cu = scan_blocks_per_cu(q.nslots, q.lds_keys > 0, r->shmem);
-  }
-  int64_t grid = (int64_t)cus * per_cu;
-  if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
-  if ((r->partitioned || r->scan_nsub > 1) && grid * kPartSub > tiles)
-    grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
-  r->grid = (int)grid;
-  if (r->partitioned) {
-    const size_t cells = (size_t)r->part.nparts * (size_t)grid * kPartCountRatio;
-    rc = r->hist.alloc(cells * 4);
-    if (!rc) rc = r->offs.alloc(cells * 8);
-    if (!rc) rc = r->part_begin.alloc(((size_t)r->part.nparts + 1) * 8);
-    if (rc) return rc;
-    r->part.hist = (uint32_t*)r->hist.p;
-    r->part.offs = (int64_t*)r->offs.p;
-    r->part.part_begin = (int64_t*)r->part_begin.p;
+    if (int rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * (size_t)std::max<int64_t>(num_keys, 1) * 8)) return rc;
   }
   HIP_OK(hipEventCreate(&r->ev0));
   HIP_OK(hipEventCreate(&r->ev1));
-  rc = run_plan(r);
-  if (rc) return rc;
+  if (int rc = run_plan(r)) return rc;
   *out = res.release();
   return 0;
 }
@@ -1819,21 +2042,34 @@ int pinot_amd_result_destroy(pinot_amd_result* r) {
   return 0;
 }
 
+static int read_counters(pinot_amd_result* r, std::vector<unsigned long long>* c) {
+  c->resize(r->matched.n / 8);
+  HIP_OK(hipMemcpyAsync(c->data(), r->matched.p, r->matched.n, hipMemcpyDeviceToHost, r->stream));
+  HIP_OK(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_docs_matched: bad arguments");
-  unsigned long long c[3];
-  HIP_OK(hipMemcpyAsync(c, r->matched.p, sizeof(c), hipMemcpyDeviceToHost, r->stream));
-  HIP_OK(hipStreamSynchronize(r->stream));
-  // partitioned plans: the count pass (skipped when the sample hands over) and the direct-atomic scan
-  // (skipped when many docs match) both count every matching doc; whichever ran has the total
-  *h_out = (int64_t)std::max(c[0], c[2]);
+  std::vector<unsigned long long> c;
+  if (int rc = read_counters(r, &c)) return rc;
+  // per launch: the scan / count pass and the direct-atomic scan both count every matching doc;
+  // whichever ran has the total (partitioned plans run one of them)
+  int64_t total = 0;
+  for (size_t li = 0; li < r->launches.size(); ++li) total += (int64_t)std::max(c[3 * li], c[3 * li + 2]);
+  *h_out = total;
   return 0;
 }
 
 const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
   if (!r) return "";
   static thread_local std::string info;
-  info = r->jit ? (r->partitioned ? "jit-partitioned" : "jit") : ("aot: " + r->jit_status);
+  switch (r->kind) {
+    case PLAN_PARTITIONED: info = "jit-partitioned"; break;
+    case PLAN_HASH: info = r->trim ? "jit-hash-trim" : "jit-hash"; break;
+    default: info = "jit";
+  }
+  if (r->launches.size() > 1) info += " x" + std::to_string(r->launches.size());
   return info.c_str();
 }
 
@@ -1846,25 +2082,90 @@ int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms) {
   return 0;
 }
 
-static int fetch_acc(pinot_amd_result* r, std::vector<uint64_t>* h) {
-  const int64_t nk = r->q.num_keys;
-  try {
-    h->resize((size_t)std::max(r->q.nacc, 1) * nk);
-  } catch (const std::bad_alloc&) {
-    return fail(PINOT_AMD_ENOMEM, "fetch: %lld accumulator slots do not fit host memory", (long long)(r->q.nacc * nk));
+// Compact the non-empty groups on the device (presence bitset -> ballot / prefix-sum compaction ->
+// gather) and copy only those rows to the host; hash-table groups are then put in key order.
+static int compact_groups(pinot_amd_result* r) {
+  if (r->compacted) return 0;
+  hipStream_t st = r->stream;
+  const int nacc = std::max(r->q.nacc, 1);
+  std::vector<unsigned long long> c;
+  if (int rc = read_counters(r, &c)) return rc;
+  if (c[3 * r->launches.size() + 1] != 0)
+    return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
+                (long long)c[3 * r->launches.size() + 1]);
+  if (r->num_group_by == 0 || r->q.nacc == 0) {
+    r->ngroups = 1;
+    r->ckeys.assign(1, 0);
+    r->cacc.assign((size_t)nacc, 0);
+    if (r->q.nacc > 0) {
+      HIP_OK(hipMemcpyAsync(r->cacc.data(), r->acc.p, (size_t)nacc * 8, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+    r->compacted = true;
+    return 0;
   }
-  if (r->q.nacc == 0) return 0;
-  HIP_OK(hipMemcpyAsync(h->data(), r->acc.p, h->size() * 8, hipMemcpyDeviceToHost, r->stream));
-  HIP_OK(hipStreamSynchronize(r->stream));
+  const bool hash = r->kind == PLAN_HASH;
+  const int64_t slots = hash ? r->fcap : r->q.num_keys;
+  const int nwk = hash ? r->nw : 1;
+  DevBuf bits, counts, total, idx, okeys, oacc;
+  if (int rc = bits.alloc((size_t)((slots + 63) / 64 + 1) * 8)) return rc;
+  HIP_OK(launch_presence_bitset((const uint64_t*)r->acc.p, slots, (unsigned long long*)bits.p, st));
+  const int64_t nc = compact_num_chunks(slots);
+  if (int rc = counts.alloc((size_t)nc * 8)) return rc;
+  if (int rc = total.alloc(8)) return rc;
+  HIP_OK(launch_bitset_count((const uint64_t*)bits.p, slots, (int64_t*)counts.p, (int64_t*)total.p, st));
+  int64_t ng = 0;
+  HIP_OK(hipMemcpyAsync(&ng, total.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  r->ngroups = ng;
+  r->ckeys.assign((size_t)ng * nwk, 0);
+  r->cacc.assign((size_t)ng * nacc, 0);
+  if (ng > 0) {
+    if (int rc = idx.alloc((size_t)ng * 4)) return rc;
+    if (int rc = okeys.alloc((size_t)ng * nwk * 8)) return rc;
+    if (int rc = oacc.alloc((size_t)ng * nacc * 8)) return rc;
+    HIP_OK(launch_bitset_compact((const uint64_t*)bits.p, slots, (const int64_t*)counts.p, (int32_t*)idx.p, st));
+    HIP_OK(launch_gather_groups((const int32_t*)idx.p, ng, hash ? (const unsigned long long*)r->fkeys.p : nullptr, nwk,
+                                slots, (const uint64_t*)r->acc.p, nacc, (uint64_t*)okeys.p, (uint64_t*)oacc.p, st));
+    HIP_OK(hipMemcpyAsync(r->ckeys.data(), okeys.p, r->ckeys.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(r->cacc.data(), oacc.p, r->cacc.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  if (hash && ng > 1) {  // ascending global key: column ids compared from the last column to the first
+    const int G = r->num_group_by;
+    std::vector<std::vector<uint32_t>> ids((size_t)ng, std::vector<uint32_t>(G));
+    for (int64_t g = 0; g < ng; ++g)
+      for (int j = 0; j < G; ++j)
+        ids[g][j] = (uint32_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) &
+                               (((uint64_t)1 << r->pack_bits[j]) - 1));
+    std::vector<int64_t> perm((size_t)ng);
+    for (int64_t g = 0; g < ng; ++g) perm[g] = g;
+    std::sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) {
+      for (int j = G - 1; j >= 0; --j)
+        if (ids[a][j] != ids[b][j]) return ids[a][j] < ids[b][j];
+      return false;
+    });
+    std::vector<uint64_t> k2(r->ckeys.size()), a2(r->cacc.size());
+    for (int64_t i = 0; i < ng; ++i) {
+      std::copy_n(&r->ckeys[(size_t)perm[i] * nwk], nwk, &k2[(size_t)i * nwk]);
+      std::copy_n(&r->cacc[(size_t)perm[i] * nacc], nacc, &a2[(size_t)i * nacc]);
+    }
+    r->ckeys.swap(k2);
+    r->cacc.swap(a2);
+  }
+  r->compacted = true;
   return 0;
 }
 
 int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_out) {
   if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_groups_limit_reached: bad arguments");
-  int64_t g = 0;
-  int rc = pinot_amd_result_num_groups(r, &g);
-  if (rc) return rc;
-  *h_out = (r->num_group_by > 0 && g > r->num_groups_limit) ? 1 : 0;
+  *h_out = 0;
+  // without a segment that can hold numGroupsLimit keys the flag is false; otherwise the trim pass
+  // computed GroupByOperator's numGroups >= numGroupsLimit per segment
+  if (r->num_group_by == 0 || !r->limit_possible) return 0;
+  std::vector<unsigned long long> c;
+  if (int rc = read_counters(r, &c)) return rc;
+  *h_out = c[3 * r->launches.size()] != 0 ? 1 : 0;
   return 0;
 }
 
@@ -1874,12 +2175,8 @@ int pinot_amd_result_num_groups(pinot_amd_result* r, int64_t* h_out) {
     *h_out = 1;
     return 0;
   }
-  std::vector<uint64_t> h;
-  int rc = fetch_acc(r, &h);
-  if (rc) return rc;
-  int64_t g = 0;
-  for (int64_t k = 0; k < r->q.num_keys; ++k) g += h[k] != 0;
-  *h_out = g;
+  if (int rc = compact_groups(r)) return rc;
+  *h_out = r->ngroups;
   return 0;
 }
 
@@ -1895,43 +2192,55 @@ static double decode_ordered(uint64_t u, int op) {
 int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, double* h_values, int64_t* h_values_i64,
                            int64_t* h_num_fetched) {
   if (!r || cap < 0 || !h_num_fetched) return fail(PINOT_AMD_EINVAL, "fetch: bad arguments");
-  std::vector<uint64_t> h;
-  int rc = fetch_acc(r, &h);
-  if (rc) return rc;
-  const int64_t nk = r->q.num_keys;
+  if (int rc = no_throw("fetch", [&] { return compact_groups(r); })) return rc;
   const int na = (int)r->agg_type.size();
-  int64_t g = 0;
-  for (int64_t k = 0; k < nk; ++k) {
-    const uint64_t cnt = r->q.nacc ? h[k] : 0;
-    if (r->num_group_by > 0 && cnt == 0) continue;
-    if (g >= cap) return fail(PINOT_AMD_EOVERFLOW, "fetch: more than %lld groups", (long long)cap);
+  const int nacc = std::max(r->q.nacc, 1);
+  const bool hash = r->kind == PLAN_HASH;
+  const int nwk = hash ? r->nw : 1;
+  if (r->ngroups > cap) return fail(PINOT_AMD_EOVERFLOW, "fetch: %lld groups exceed capacity %lld", (long long)r->ngroups,
+                                    (long long)cap);
+  for (int64_t g = 0; g < r->ngroups; ++g) {
+    const uint64_t* A = &r->cacc[(size_t)g * nacc];
+    const uint64_t cnt = r->q.nacc ? A[0] : 0;
     if (h_keys) {
-      int64_t rem = k;
+      int64_t rem = hash ? 0 : (int64_t)r->ckeys[(size_t)g];
       for (int j = 0; j < r->num_group_by; ++j) {
         const MergedKeyColumn& m = r->keys[j];
-        const int64_t sz = (int64_t)std::max<size_t>(m.size(), 1);
-        const int64_t id = rem % sz;
-        rem /= sz;
-        int64_t out;
-        if (m.type == T_STRING) out = id;
-        else if (is_float(m.type)) memcpy(&out, &m.vd[id], 8);
-        else out = m.vi[id];
-        h_keys[g * r->num_group_by + j] = out;
+        int64_t id;
+        if (hash) {
+          id = (int64_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) & (((uint64_t)1 << r->pack_bits[j]) - 1));
+        } else {
+          const int64_t sz = (int64_t)std::max<size_t>(m.size(), 1);
+          id = rem % sz;
+          rem /= sz;
+        }
+        int64_t o;
+        if (m.type == T_STRING) o = id;
+        else if (is_float(m.type)) memcpy(&o, &m.vd[id], 8);
+        else o = m.vi[id];
+        h_keys[g * r->num_group_by + j] = o;
       }
     }
     for (int a = 0; a < na; ++a) {
       const int acc = r->agg_acc[a];
       const int op = r->q.acc_op[acc];
-      const uint64_t w = h[(size_t)acc * nk + k];
+      const uint64_t w = A[acc];
       double v;
       int64_t vi = 0;
+      // exact 128-bit integer sum (lo, hi) -> correctly rounded double
+      auto sum128 = [&](int64_t* exact) -> double {
+        const __int128 s = (__int128)(((unsigned __int128)A[acc + 1] << 64) | (unsigned __int128)w);
+        *exact = (s >= (__int128)INT64_MIN && s <= (__int128)INT64_MAX) ? (int64_t)s : INT64_MIN;
+        return (double)s;
+      };
       switch (r->agg_type[a]) {
         case PINOT_AMD_AGG_COUNT:
           vi = (int64_t)cnt;
           v = (double)vi;
           break;
         case PINOT_AMD_AGG_AVG: {
-          const double s = op == ACC_SUM_F64 ? ([&] { double d; memcpy(&d, &w, 8); return d; })() : (double)(int64_t)w;
+          int64_t ex;
+          const double s = op == ACC_SUM_F64 ? ([&] { double d; memcpy(&d, &w, 8); return d; })() : sum128(&ex);
           v = cnt ? s / (double)cnt : -INFINITY;  // AvgAggregationFunction: empty -> DEFAULT_FINAL_RESULT
           break;
         }
@@ -1942,6 +2251,8 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
         default:
           if (op == ACC_SUM_F64) {
             memcpy(&v, &w, 8);
+          } else if (op == ACC_SUM_I128) {
+            v = sum128(&vi);
           } else {
             vi = (int64_t)w;
             v = (double)vi;
@@ -1950,9 +2261,8 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
       if (h_values) h_values[g * na + a] = v;
       if (h_values_i64) h_values_i64[g * na + a] = vi;
     }
-    ++g;
   }
-  *h_num_fetched = g;
+  *h_num_fetched = r->ngroups;
   return 0;
 }
 
@@ -1966,13 +2276,21 @@ const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t 
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops) {
   if (!r || !h_num_slots || !h_num_key_slots) return fail(PINOT_AMD_EINVAL, "accumulators: bad arguments");
+  if (r->kind == PLAN_HASH)
+    return fail(PINOT_AMD_EUNSUPPORTED, "accumulators: hash-table results merge by value (pinot_amd_result_fetch)");
   *h_num_slots = r->q.nacc;
   *h_num_key_slots = r->q.num_keys;
   for (int a = 0; a < r->q.nacc; ++a) {
     if (h_slot_ptrs) h_slot_ptrs[a] = (uint8_t*)r->acc.p + (size_t)a * r->q.num_keys * 8;
     if (h_slot_ops) {
-      const int op = r->q.acc_op[a];
-      h_slot_ops[a] = (op == ACC_COUNT || op == ACC_SUM_I64) ? 0 : op == ACC_SUM_F64 ? 1 : op == ACC_MIN ? 2 : 3;
+      switch (r->q.acc_op[a]) {
+        case ACC_SUM_F64: h_slot_ops[a] = 1; break;
+        case ACC_MIN: h_slot_ops[a] = 2; break;
+        case ACC_MAX: h_slot_ops[a] = 3; break;
+        case ACC_SUM_I128: h_slot_ops[a] = 4; break;
+        case ACC_HI: h_slot_ops[a] = 5; break;
+        default: h_slot_ops[a] = 0;  // COUNT, SUM_I64
+      }
     }
   }
   return 0;

@@ -36,7 +36,7 @@ struct JitVal {
   bool operator==(const JitVal& o) const { return expr == o.expr && slot == o.slot && slot2 == o.slot2; }
 };
 struct JitAcc {
-  int op;    // ACC_*
+  int op;    // ACC_* (an ACC_SUM_I128 is followed by its ACC_HI entry; ACC_FIRST_DOC reads no slot)
   int slot;
   int expr = EXPR_COL;
   int slot2 = -1;
@@ -68,6 +68,12 @@ struct JitPlan {
   std::vector<int> val_off;    // byte offset of each value column in a record (key u32 at 0)
   int rec_bytes = 0;           // record size, multiple of 8
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
+  // hash-table GROUP BY (DevHash): group column j's merged id goes to key word hash_pack[j].first at
+  // bit hash_pack[j].second; hash_seg appends the segment's key_seg as the last word (trimming)
+  bool hash = false;
+  int hash_words = 0;          // key words including the segment word
+  bool hash_seg = false;
+  std::vector<std::pair<int, int>> hash_pack;
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals)
 void jit_layout_records(JitPlan* p);

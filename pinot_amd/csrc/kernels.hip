@@ -4,11 +4,10 @@
 // forward index as the big-endian MSB-first bit stream, raw values big-endian — so nothing is
 // transcoded at staging time; the kernels byte-swap in registers (v_perm_b32).
 //
-// Work decomposition: a block of 256 threads (4 wave64) owns a contiguous range of 1024-doc tiles
-// across the whole segment batch; each lane owns 4 consecutive docs of a tile, so a raw INT column
-// is one 16 B load per lane (1 KiB per wave instruction, fully coalesced) and a LONG/DOUBLE column
-// two. Filter, group-key and aggregation are fused in one pass; group accumulators live in LDS
-// when the key space fits and are merged into HBM with atomics once per block.
+// The fused scan (filter + group key + aggregation) is generated per query shape and compiled with
+// hipRTC (jit.cpp); this file holds the fixed kernels around it: accumulator initialisation, the
+// hash-table trimming / merge / result compaction passes, the low-level operators (forward-index
+// decode, bitsets, docId compaction), inverted-index expansion and raw-chunk decompression.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,10 +24,6 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 __device__ __forceinline__ uint64_t bswap64(uint32_t hi_word_be, uint32_t lo_word_be) {
   // bytes as stored: hi_word_be holds the first 4 bytes (most significant in BE order)
   return ((uint64_t)bswap32(hi_word_be) << 32) | bswap32(lo_word_be);
-}
-__device__ __forceinline__ uint64_t ordered_from_double(double d) {
-  uint64_t u = (uint64_t)__double_as_longlong(d);
-  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 __device__ __forceinline__ double u64_as_double(uint64_t u) { return __longlong_as_double((long long)u); }
 
@@ -54,172 +49,6 @@ __device__ __forceinline__ void load_fixed_bit4(const uint8_t* data, int bits, i
   }
 }
 
-// dictId of a doc of a sorted column: last dictId whose first doc <= doc (SortedIndexReaderImpl).
-__device__ __forceinline__ int32_t sorted_dict_id(const int32_t* starts, int32_t card, int64_t doc) {
-  int32_t lo = 0, hi = card - 1;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi + 1) >> 1;
-    if ((int64_t)starts[mid] <= doc) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-// A lane's raw words for one column of one tile: fetched early (prefetch), decoded later.
-struct Raw {
-  uint4 a, b;
-};
-
-// Issue the loads of a column's 4 docs at doc0: fixed-bit = 5-dword window, raw 4 B = one 16 B
-// load, raw 8 B = two 16 B loads. Sorted columns are decoded by dependent lookups (no fetch).
-// Every path assigns both vectors whole so the words stay in registers.
-__device__ __forceinline__ Raw fetch_slot(const DevColumn& c, int64_t doc0) {
-  Raw r;
-  if (c.enc == ENC_FIXED_BIT) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(c.data) + ((doc0 * c.bits) >> 5);
-    r.a = make_uint4(w[0], w[1], w[2], w[3]);
-    r.b = make_uint4(w[4], 0u, 0u, 0u);
-  } else if (c.enc == ENC_RAW) {
-    if (c.type == T_INT || c.type == T_FLOAT) {
-      r.a = *reinterpret_cast<const uint4*>(c.data + doc0 * 4);
-      r.b = make_uint4(0u, 0u, 0u, 0u);
-    } else {
-      r.a = *reinterpret_cast<const uint4*>(c.data + doc0 * 8);
-      r.b = *reinterpret_cast<const uint4*>(c.data + doc0 * 8 + 16);
-    }
-  } else {
-    r.a = make_uint4(0u, 0u, 0u, 0u);
-    r.b = r.a;
-  }
-  return r;
-}
-
-// Decoded per-slot representation: dictIds (dict columns), INT/LONG values, or FLOAT/DOUBLE as
-// double bits.
-__device__ __forceinline__ void decode_slot(const DevColumn& c, int64_t doc0, const Raw& r, int64_t v[4]) {
-  if (c.enc == ENC_FIXED_BIT) {
-    const int bits = c.bits;
-    const uint32_t rr = (uint32_t)((doc0 * bits) & 31);
-    const uint32_t x0 = bswap32(r.a.x), x1 = bswap32(r.a.y), x2 = bswap32(r.a.z), x3 = bswap32(r.a.w),
-                   x4 = bswap32(r.b.x);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t p = rr + (uint32_t)(k * bits);
-      const uint32_t i = p >> 5, sh = p & 31;
-      const uint64_t win = ((uint64_t)sel4(i, x0, x1, x2, x3) << 32) | sel4(i, x1, x2, x3, x4);
-      v[k] = (int64_t)((win << sh) >> (64 - bits));
-    }
-  } else if (c.enc == ENC_RAW) {
-    if (c.type == T_INT) {
-      v[0] = (int64_t)(int32_t)bswap32(r.a.x);
-      v[1] = (int64_t)(int32_t)bswap32(r.a.y);
-      v[2] = (int64_t)(int32_t)bswap32(r.a.z);
-      v[3] = (int64_t)(int32_t)bswap32(r.a.w);
-    } else if (c.type == T_FLOAT) {
-      v[0] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.x)));
-      v[1] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.y)));
-      v[2] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.z)));
-      v[3] = __double_as_longlong((double)__uint_as_float(bswap32(r.a.w)));
-    } else {
-      v[0] = (int64_t)bswap64(r.a.x, r.a.y);
-      v[1] = (int64_t)bswap64(r.a.z, r.a.w);
-      v[2] = (int64_t)bswap64(r.b.x, r.b.y);
-      v[3] = (int64_t)bswap64(r.b.z, r.b.w);
-    }
-  } else {  // ENC_SORTED
-    const int32_t* starts = reinterpret_cast<const int32_t*>(c.data);
-    int32_t id = sorted_dict_id(starts, c.card, doc0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      while (id + 1 < c.card && (int64_t)starts[id + 1] <= doc0 + k) ++id;
-      v[k] = id;
-    }
-  }
-}
-
-// value of slot element as int64 (for SUM on integer columns) — dict columns go through the
-// dictionary (BlockValSet.getLongValuesSV over Dictionary.readLongValues)
-__device__ __forceinline__ int64_t slot_value_i64(const DevColumn& c, int64_t x) {
-  if (c.enc == ENC_RAW) return x;
-  return c.type == T_INT ? (int64_t) reinterpret_cast<const int32_t*>(c.dict)[x]
-                         : reinterpret_cast<const int64_t*>(c.dict)[x];
-}
-// value as double (SUM on FLOAT/DOUBLE, MIN, MAX: Pinot aggregates these in double)
-__device__ __forceinline__ double slot_value_f64(const DevColumn& c, int64_t x) {
-  if (c.enc == ENC_RAW) {
-    return (c.type == T_INT || c.type == T_LONG) ? (double)x : __longlong_as_double(x);
-  }
-  switch (c.type) {
-    case T_INT: return (double)reinterpret_cast<const int32_t*>(c.dict)[x];
-    case T_LONG: return (double)reinterpret_cast<const int64_t*>(c.dict)[x];
-    case T_FLOAT: return (double)reinterpret_cast<const float*>(c.dict)[x];
-    default: return reinterpret_cast<const double*>(c.dict)[x];
-  }
-}
-
-__device__ __forceinline__ bool in_sorted_i64(const int64_t* a, int32_t n, int64_t v) {
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo < n && a[lo] == v;
-}
-__device__ __forceinline__ bool in_sorted_f64(const double* a, int32_t n, double v) {
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo < n && a[lo] == v;
-}
-
-// one predicate leaf over the lane's 4 docs -> 4-bit mask
-__device__ __forceinline__ uint32_t eval_leaf(const DevLeaf& L, const int64_t v[4], int64_t doc0) {
-  uint32_t m = 0;
-  switch (L.kind) {
-    case LEAF_DICT_RANGE:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= (uint32_t)(v[k] >= L.lo_i && v[k] < L.hi_i) << k;
-      break;
-    case LEAF_DICT_SET:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= ((L.bits[v[k] >> 5] >> (v[k] & 31)) & 1u) << k;
-      break;
-    case LEAF_RAW_RANGE_I:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= (uint32_t)(v[k] >= L.lo_i && v[k] <= L.hi_i) << k;
-      break;
-    case LEAF_RAW_RANGE_F:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double d = __longlong_as_double(v[k]);
-        m |= (uint32_t)(d >= L.lo_d && d <= L.hi_d) << k;
-      }
-      break;
-    case LEAF_RAW_IN_I:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= (uint32_t)in_sorted_i64(L.in_i, L.in_n, v[k]) << k;
-      break;
-    case LEAF_RAW_IN_F:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= (uint32_t)in_sorted_f64(L.in_d, L.in_n, __longlong_as_double(v[k])) << k;
-      break;
-    case LEAF_DOC_RANGE:
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m |= (uint32_t)(doc0 + k >= L.lo_i && doc0 + k <= L.hi_i) << k;
-      break;
-    case LEAF_DOC_BITSET: {
-      // doc0 is a multiple of 4: the 4 bits sit in one 32-bit word
-      m = (L.bits[doc0 >> 5] >> (doc0 & 31)) & 0xFu;
-      break;
-    }
-    default:  // LEAF_CONST
-      m = L.lo_i ? 0xFu : 0u;
-      break;
-  }
-  return L.negate ? (~m & 0xFu) : m;
-}
-
 // ------------------------------------------------------------------------------------------------
 // wave reductions (64 lanes)
 // ------------------------------------------------------------------------------------------------
@@ -228,288 +57,228 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
 }
-__device__ __forceinline__ double wave_sum_f64(double x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t y = __shfl_xor(x, o, 64);
-    x = y < x ? y : x;
-  }
-  return x;
-}
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t y = __shfl_xor(x, o, 64);
-    x = y > x ? y : x;
-  }
-  return x;
-}
-
-// accumulator update at a table word (LDS or HBM; generic address space resolves both)
-__device__ __forceinline__ void acc_apply(int32_t op, uint64_t* p, uint64_t bits) {
+// accumulator update at a table word (LDS or HBM; generic address space resolves both); an
+// ACC_SUM_I128 low word carries into `hi` (the next array's word)
+__device__ __forceinline__ void acc_apply(int32_t op, uint64_t* p, uint64_t* hi, uint64_t bits, uint64_t hbits) {
   switch (op) {
     case ACC_COUNT:
     case ACC_SUM_I64:
       atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
       break;
+    case ACC_SUM_I128: {
+      const uint64_t old = (uint64_t)atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+      const uint64_t h = hbits + (uint64_t)(old + bits < old);
+      if (h) atomicAdd(reinterpret_cast<unsigned long long*>(hi), (unsigned long long)h);
+      break;
+    }
+    case ACC_HI:
+      break;
     case ACC_SUM_F64:
       unsafeAtomicAdd(reinterpret_cast<double*>(p), u64_as_double(bits));
       break;
-    case ACC_MIN:
-      atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
-      break;
-    default:
+    case ACC_MAX:
       atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
+      break;
+    default:  // ACC_MIN, ACC_FIRST_DOC
+      atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)bits);
       break;
   }
 }
 
 __device__ __forceinline__ uint64_t acc_identity(int32_t op) {
-  if (op == ACC_MIN) return ~0ull;
+  if (op == ACC_MIN || op == ACC_FIRST_DOC) return ~0ull;
   return 0ull;  // COUNT/SUM: 0 (also +0.0 for f64); MAX: ordered 0 is below every double
-}
-
-// ------------------------------------------------------------------------------------------------
-// Fused filter + group-by + aggregation over a batch of segments.
-//   kBitset: also write the filter's docId bitset (per segment, at bitset_out[s] words)
-//   kLds:    accumulate into an LDS-privatised table of q.lds_keys keys, flushed once per block
-// ------------------------------------------------------------------------------------------------
-template <int NS, bool kLds, bool kBitset>
-__global__ void __launch_bounds__(kBlock) scan_kernel(const DevSegment* __restrict__ segs, const DevQuery q,
-                                                      uint64_t* __restrict__ acc,      // [nacc][num_keys]
-                                                      uint64_t* const* __restrict__ bitset_out,
-                                                      unsigned long long* __restrict__ matched_out) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds_table[];  // [nacc][lds_keys]
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-
-  if constexpr (kLds) {
-    const int n = q.nacc * q.lds_keys;
-    for (int i = tid; i < n; i += kBlock) lds_table[i] = acc_identity(q.acc_op[i / q.lds_keys]);
-    __syncthreads();
-  }
-  uint64_t* const table = kLds ? lds_table : acc;
-  const int64_t tstride = kLds ? (int64_t)q.lds_keys : q.num_keys;
-
-  // contiguous tile range of this block
-  const int64_t per = (q.total_tiles + gridDim.x - 1) / gridDim.x;
-  const int64_t t_begin = (int64_t)blockIdx.x * per;
-  const int64_t t_end = min(q.total_tiles, t_begin + per);
-  int64_t matched = 0;
-
-  int s = 0;
-  if (t_begin < t_end) {
-    // last segment whose tile_begin <= t_begin (wave-uniform binary search)
-    int lo = 0, hi = q.nsegs - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (segs[mid].tile_begin <= t_begin) lo = mid; else hi = mid - 1;
-    }
-    s = lo;
-  }
-
-  auto doc_of = [&](int seg_idx, int64_t t) -> int64_t {
-    return (t - segs[seg_idx].tile_begin) * kTileDocs + (int64_t)tid * kDocsPerThread;
-  };
-  // software pipeline: the next tile's column words are in flight while this tile is processed
-  Raw rc[NS];
-#pragma unroll
-  for (int sl = 0; sl < NS; ++sl) {
-    rc[sl].a = make_uint4(0u, 0u, 0u, 0u);
-    rc[sl].b = rc[sl].a;
-    if (t_begin < t_end && sl < q.nslots) rc[sl] = fetch_slot(segs[s].cols[sl], doc_of(s, t_begin));
-  }
-
-  for (int64_t t = t_begin; t < t_end; ++t) {
-    const DevSegment& seg = segs[s];
-    const int64_t doc0 = doc_of(s, t);
-    const int64_t nd = seg.num_docs;
-    uint32_t match = doc0 + 4 <= nd ? 0xFu : doc0 >= nd ? 0u : (0xFu >> (4 - (nd - doc0)));
-
-    int s_next = s;
-    while (s_next + 1 < q.nsegs && segs[s_next + 1].tile_begin <= t + 1) ++s_next;
-    Raw rn[NS];
-    const int64_t doc_n = doc_of(s_next, t + 1);
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      rn[sl].a = make_uint4(0u, 0u, 0u, 0u);
-      rn[sl].b = rn[sl].a;
-      if (t + 1 < t_end && sl < q.nslots) rn[sl] = fetch_slot(segs[s_next].cols[sl], doc_n);
-    }
-
-    // ---- decode every referenced column (compile-time slot indices only) ----
-    int64_t v[NS][4];
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      if (sl < q.nslots) decode_slot(seg.cols[sl], doc0, rc[sl], v[sl]);
-    }
-
-    // ---- filter: AND over clauses of OR over leaves ----
-    if (q.nleaves > 0) {
-      uint64_t clause_bits = 0;
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        if (sl < q.nslots) {
-          for (int l = q.slot_leaf_begin[sl]; l < q.slot_leaf_begin[sl + 1]; ++l) {
-            const DevLeaf& L = seg.leaves[l];
-            clause_bits |= (uint64_t)eval_leaf(L, v[sl], doc0) << (4 * L.clause);
-          }
-        }
-      }
-      for (int l = q.slotless_leaf_begin; l < q.slotless_leaf_end; ++l) {
-        const DevLeaf& L = seg.leaves[l];
-        clause_bits |= (uint64_t)eval_leaf(L, v[0], doc0) << (4 * L.clause);
-      }
-      for (int c = 0; c < q.nclauses; ++c) match &= (uint32_t)(clause_bits >> (4 * c)) & 0xFu;
-    }
-
-    if constexpr (kBitset) {
-      // lane l holds bits for docs doc0..doc0+3 = bits 4*(l%16).. of word (tile*16 + tid/16)
-      uint64_t w = (uint64_t)match << (4 * (lane & 15));
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) w |= __shfl_xor(w, o, 64);
-      if ((lane & 15) == 0) bitset_out[s][(doc0 >> 6)] = w;
-    }
-
-    matched += __builtin_popcount(match);
-    do {  // aggregation; `break` leaves it, the pipeline rotation below always runs
-    if (q.nacc == 0) break;
-
-    // ---- group key per doc ----
-    int64_t key[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      if (sl < q.nslots && q.slot_group_stride[sl] > 0) {
-        const int32_t* remap = seg.cols[sl].remap;
-        const int64_t st = q.slot_group_stride[sl];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) key[k] += (int64_t)(remap ? remap[v[sl][k]] : (int32_t)v[sl][k]) * st;
-      }
-    }
-
-    // ---- aggregation ----
-    // wave-uniform key fast path: every matching doc of the wave falls in one group (always true
-    // for aggregation-only queries; common for sorted time columns)
-    const bool lane_has = match != 0;
-    const int first_k = lane_has ? __builtin_ctz(match) : 0;
-    const int64_t kA = key[first_k];
-    bool lane_uniform = true;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lane_uniform &= !((match >> k) & 1) || key[k] == kA;
-    const unsigned long long has_mask = __ballot(lane_has);
-    if (has_mask == 0) break;
-    const int src = __ffsll((long long)has_mask) - 1;
-    const int64_t kW = __shfl(kA, src, 64);
-    const bool wave_uniform = __ballot(lane_has && (!lane_uniform || kA != kW)) == 0;
-
-    if (wave_uniform) {
-      uint64_t* row = table + kW;
-      const int64_t cnt = wave_sum_i64(__builtin_popcount(match));
-      if (lane == 0) acc_apply(ACC_COUNT, row, (uint64_t)cnt);
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        if (sl < q.nslots) {
-          const DevColumn& col = seg.cols[sl];
-          for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
-            const int32_t op = q.acc_op[a];
-            uint64_t r;
-            if (op == ACC_SUM_I64) {
-              int64_t p = 0;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) p += ((match >> k) & 1) ? slot_value_i64(col, v[sl][k]) : 0;
-              r = (uint64_t)wave_sum_i64(p);
-            } else if (op == ACC_SUM_F64) {
-              double p = 0.0;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) p += ((match >> k) & 1) ? slot_value_f64(col, v[sl][k]) : 0.0;
-              r = (uint64_t)__double_as_longlong(wave_sum_f64(p));
-            } else if (op == ACC_MIN) {
-              uint64_t p = ~0ull;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const double d = slot_value_f64(col, v[sl][k]);
-                // NaN: skipped by the group-by `value < min`, ordered below everything (decodes
-                // back to NaN) for aggregation-only Math.min
-                const uint64_t o = d == d ? ordered_from_double(d) : q.agg_only ? 0ull : ~0ull;
-                if (((match >> k) & 1) && o < p) p = o;
-              }
-              r = wave_min_u64(p);
-            } else {
-              uint64_t p = 0;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const double d = slot_value_f64(col, v[sl][k]);
-                const uint64_t o = d == d ? ordered_from_double(d) : q.agg_only ? ~0ull : 0ull;
-                if (((match >> k) & 1) && o > p) p = o;
-              }
-              r = wave_max_u64(p);
-            }
-            if (lane == 0) acc_apply(op, row + (int64_t)a * tstride, r);
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if ((match >> k) & 1) {
-          uint64_t* row = table + key[k];
-          acc_apply(ACC_COUNT, row, 1);
-#pragma unroll
-          for (int sl = 0; sl < NS; ++sl) {
-            if (sl < q.nslots) {
-              const DevColumn& col = seg.cols[sl];
-              for (int a = q.slot_acc_begin[sl]; a < q.slot_acc_begin[sl + 1]; ++a) {
-                const int32_t op = q.acc_op[a];
-                uint64_t r;
-                if (op == ACC_SUM_I64) {
-                  r = (uint64_t)slot_value_i64(col, v[sl][k]);
-                } else {
-                  const double d = slot_value_f64(col, v[sl][k]);
-                  if (op != ACC_SUM_F64 && d != d) {
-                    if (!q.agg_only) continue;  // group-by MIN/MAX skip NaN (`value < min`)
-                    r = op == ACC_MIN ? 0ull : ~0ull;  // Math.min/max propagate NaN
-                  } else {
-                    r = op == ACC_SUM_F64 ? (uint64_t)__double_as_longlong(d) : ordered_from_double(d);
-                  }
-                }
-                acc_apply(op, row + (int64_t)a * tstride, r);
-              }
-            }
-          }
-        }
-      }
-    }
-    } while (0);
-
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) rc[sl] = rn[sl];
-    s = s_next;
-  }
-
-  // ---- per-block results ----
-  {
-    const int64_t wm = wave_sum_i64(matched);
-    if (lane == 0 && wm) atomicAdd(matched_out, (unsigned long long)wm);
-  }
-  if constexpr (kLds) {
-    __syncthreads();
-    for (int g = tid; g < q.lds_keys; g += kBlock) {
-      if (lds_table[g] == 0) continue;  // no matching doc in this block for key g
-      for (int a = 0; a < q.nacc; ++a)
-        acc_apply(q.acc_op[a], acc + (int64_t)a * q.num_keys + g, lds_table[(int64_t)a * q.lds_keys + g]);
-    }
-  }
 }
 
 __global__ void init_acc_kernel(uint64_t* acc, int64_t num_keys, DevQuery q) {
   const int64_t n = (int64_t)q.nacc * num_keys;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     acc[i] = acc_identity(q.acc_op[i / num_keys]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hash-table GROUP BY passes (DevHash layout; the scan itself is the JIT kernel)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+// slot of the nw-word key kw in a table (inserted if absent; lock-free word-by-word CAS, see
+// DevHash), -1 when every slot holds another key
+__device__ int64_t hash_find_rt(unsigned long long* keys, int64_t cap, int nw, const uint64_t* kw) {
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (int w = 0; w < nw; ++w) x = fmix64(x ^ kw[w]);
+  const uint64_t mask = (uint64_t)cap - 1ull;
+  uint64_t i = x & mask;
+  for (int64_t n = 0; n < cap; ++n) {
+    bool ok = true;
+    for (int w = 0; w < nw && ok; ++w) {
+      unsigned long long* pw = keys + (uint64_t)w * (uint64_t)cap + i;
+      unsigned long long cur = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == ~0ull) {
+        cur = atomicCAS(pw, ~0ull, (unsigned long long)kw[w]);
+        if (cur == ~0ull) cur = kw[w];
+      }
+      ok = cur == kw[w];
+    }
+    if (ok) return (int64_t)i;
+    i = (i + 1ull) & mask;
+  }
+  return -1;
+}
+
+// numGroupsLimit trimming (DictionaryBasedGroupKeyGenerator.java:351-363 / the map holders'
+// getGroupId(rawKey, numGroupsLimit)): within a segment Pinot admits group keys in the order their
+// first matching doc appears, until numGroupsLimit keys are held; later keys are dropped. The trim
+// scan table is keyed by (key, segment) and tracks each entry's first matching docId; first docIds
+// of one segment are distinct (one key per doc), so the admitted keys are exactly those whose first
+// docId is <= the limit-th smallest first docId of the segment (dstar). Found in four passes:
+//   1. per segment: distinct entries, and a histogram of first docIds in 1024-doc buckets
+//   2. per segment: the bucket holding the limit-th first docId and its rank inside the bucket
+//   3. the first docIds of that bucket as a 1024-bit map
+//   4. the rank-th set bit -> dstar
+__global__ void trim_count_kernel(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc,
+                                  int fd_acc, const int64_t* bucket_base, uint32_t* hist,
+                                  unsigned long long* seg_distinct) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    if (acc[i] == 0ull) continue;
+    const int64_t s = (int64_t)keys[(uint64_t)(nw_seg - 1) * (uint64_t)cap + i];
+    const uint64_t fd = acc[(uint64_t)fd_acc * (uint64_t)cap + i];
+    atomicAdd(&seg_distinct[s], 1ull);
+    atomicAdd(&hist[bucket_base[s] + (int64_t)(fd >> 10)], 1u);
+  }
+}
+
+// one block per segment; bstar[s] = -1: the segment holds <= limit keys (nothing trimmed)
+__global__ void __launch_bounds__(256) trim_select_kernel(int64_t limit, const int64_t* bucket_base,
+                                                          const uint32_t* hist, const unsigned long long* seg_distinct,
+                                                          int64_t* bstar, int64_t* rank,
+                                                          unsigned long long* limit_reached) {
+  __shared__ int64_t wtot[4];
+  __shared__ int64_t carry;
+  const int s = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nd = (int64_t)seg_distinct[s];
+  // GroupByOperator.java:133: numGroupsLimitReached = numGroups >= numGroupsLimit
+  if (threadIdx.x == 0 && nd >= limit) atomicOr(limit_reached, 1ull);
+  if (nd <= limit) {
+    if (threadIdx.x == 0) bstar[s] = -1;
+    return;
+  }
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int64_t b0 = bucket_base[s], b1 = bucket_base[s + 1];
+  for (int64_t base = b0; base < b1; base += 256) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t x = i < b1 ? (int64_t)hist[i] : 0;
+    int64_t incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int w = 0; w < wave; ++w) before += wtot[w];
+    const int64_t c_incl = before + incl, c_excl = c_incl - x;
+    if (i < b1 && c_excl < limit && c_incl >= limit) {
+      bstar[s] = i - b0;
+      rank[s] = limit - c_excl;  // 1-based rank of dstar among the bucket's first docIds
+    }
+    __syncthreads();
+    if (threadIdx.x == 255) carry = c_incl;
+    __syncthreads();
+    if (carry >= limit) break;
+  }
+}
+
+__global__ void trim_bitmap_kernel(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc,
+                                   int fd_acc, const int64_t* bstar, unsigned long long* bitmap) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    if (acc[i] == 0ull) continue;
+    const int64_t s = (int64_t)keys[(uint64_t)(nw_seg - 1) * (uint64_t)cap + i];
+    const uint64_t fd = acc[(uint64_t)fd_acc * (uint64_t)cap + i];
+    if (bstar[s] >= 0 && (int64_t)(fd >> 10) == bstar[s])
+      atomicOr(&bitmap[s * 16 + (int64_t)((fd & 1023) >> 6)], 1ull << (fd & 63));
+  }
+}
+
+__global__ void trim_cutoff_kernel(int32_t nsegs, const int64_t* bstar, const int64_t* rank,
+                                   const unsigned long long* bitmap, int64_t* dstar) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  if (bstar[s] < 0) {
+    dstar[s] = INT64_MAX;
+    return;
+  }
+  int64_t r = rank[s];
+  int64_t out = -1;
+  for (int w = 0; w < 16 && out < 0; ++w) {
+    uint64_t m = bitmap[(int64_t)s * 16 + w];
+    const int c = __popcll(m);
+    if (r > c) {
+      r -= c;
+      continue;
+    }
+    while (--r > 0) m &= m - 1;
+    out = bstar[s] * 1024 + w * 64 + __builtin_ctzll(m);
+  }
+  dstar[s] = out;
+}
+
+// Fold a scan table into the final table: every present entry (admitted by the trim cutoff when
+// dstar != nullptr; the segment word is dropped from the key) is inserted by key and its
+// accumulators applied with the plan's ops (AggregationFunction.merge of the combine).
+__global__ void hash_merge_kernel(const unsigned long long* skeys, int64_t scap, int nw, int has_seg,
+                                  const uint64_t* sacc, unsigned long long* fkeys, int64_t fcap, uint64_t* facc,
+                                  DevQuery q, int fd_acc, const int64_t* dstar, unsigned long long* overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < scap; i += (int64_t)gridDim.x * blockDim.x) {
+    if (sacc[i] == 0ull) continue;
+    if (dstar) {
+      const int64_t s = (int64_t)skeys[(uint64_t)nw * (uint64_t)scap + i];
+      if (sacc[(uint64_t)fd_acc * (uint64_t)scap + i] > (uint64_t)dstar[s]) continue;
+    }
+    uint64_t kw[kMaxKeyWords];
+    for (int w = 0; w < nw; ++w) kw[w] = skeys[(uint64_t)w * (uint64_t)scap + i];
+    const int64_t slot = hash_find_rt(fkeys, fcap, nw, kw);
+    if (slot < 0) {
+      atomicAdd(overflow, 1ull);
+      continue;
+    }
+    for (int a = 0; a < q.nacc; ++a) {
+      const uint64_t v = sacc[(uint64_t)a * (uint64_t)scap + i];
+      const uint64_t vh = a + 1 < q.nacc ? sacc[(uint64_t)(a + 1) * (uint64_t)scap + i] : 0ull;
+      acc_apply(q.acc_op[a], facc + (uint64_t)a * (uint64_t)fcap + slot,
+                facc + (uint64_t)(a + 1 < q.nacc ? a + 1 : a) * (uint64_t)fcap + slot, v, vh);
+    }
+    (void)has_seg;
+  }
+}
+
+// Result compaction (GroupKeyGenerator.getGroupKeys on the device): bit i of `bits` = table slot i
+// holds a group (its COUNT accumulator is non-zero); one wave ballot per 64 slots.
+__global__ void presence_bitset_kernel(const uint64_t* count, int64_t n, unsigned long long* bits) {
+  const int64_t nw = (n + 63) / 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw * 64; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool present = i < n && count[i] != 0ull;
+    const unsigned long long m = __ballot(present);
+    if ((threadIdx.x & 63) == 0) bits[i >> 6] = m;
+  }
+}
+
+// gather the compacted groups: key words (hash tables) and every accumulator word, row-major
+__global__ void gather_groups_kernel(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
+                                     int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys,
+                                     uint64_t* out_acc) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t slot = (uint64_t)(uint32_t)slots[g];
+    for (int w = 0; w < nw; ++w) out_keys[g * nw + w] = keys ? keys[(uint64_t)w * (uint64_t)cap + slot] : slot;
+    for (int a = 0; a < nacc; ++a) out_acc[g * nacc + a] = acc[(uint64_t)a * (uint64_t)cap + slot];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1007,60 +776,54 @@ hipError_t launch_chunk_decompress(const uint8_t* src, uint8_t* dst, const void*
   return hipGetLastError();
 }
 
-template <int NS>
-static hipError_t launch_scan_ns(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc,
-                                 uint64_t* const* d_bitsets, unsigned long long* d_matched, int grid, size_t shmem,
-                                 hipStream_t st) {
-  if (d_bitsets)  // filter-only plan (FilterPlanNode -> docId set): no accumulators
-    hipLaunchKernelGGL((scan_kernel<NS, false, true>), dim3(grid), dim3(kBlock), 0, st, d_segs, q, d_acc, d_bitsets,
-                       d_matched);
-  else if (q.lds_keys > 0)
-    hipLaunchKernelGGL((scan_kernel<NS, true, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc, nullptr,
-                       d_matched);
-  else
-    hipLaunchKernelGGL((scan_kernel<NS, false, false>), dim3(grid), dim3(kBlock), shmem, st, d_segs, q, d_acc,
-                       nullptr, d_matched);
+hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st) {
+  const int64_t n = (int64_t)q.nacc * num_keys;
+  unsigned g = grid_for(n, kBlock);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(init_acc_kernel, dim3(g), dim3(kBlock), 0, st, d_acc, num_keys, q);
   return hipGetLastError();
 }
 
-// slot-count variant: decoded values live in NS x 4 registers, so a 4-column query does not pay
-// the register cost (and occupancy) of the 8-column kernel
-static inline int ns_for(int nslots) { return nslots <= 1 ? 1 : nslots <= 2 ? 2 : nslots <= 4 ? 4 : 8; }
-
-hipError_t launch_scan(const DevSegment* d_segs, const DevQuery& q, uint64_t* d_acc, uint64_t* const* d_bitsets,
-                       unsigned long long* d_matched, int grid, hipStream_t st) {
-  const size_t shmem = q.lds_keys > 0 ? (size_t)q.nacc * q.lds_keys * 8 : 0;
-  if (d_bitsets && q.nacc > 0) return hipErrorNotSupported;
-  switch (ns_for(q.nslots)) {
-    case 1: return launch_scan_ns<1>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
-    case 2: return launch_scan_ns<2>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
-    case 4: return launch_scan_ns<4>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
-    default: return launch_scan_ns<8>(d_segs, q, d_acc, d_bitsets, d_matched, grid, shmem, st);
-  }
+static inline unsigned grid_cap(int64_t n, int per_block, unsigned cap) {
+  const unsigned g = grid_for(n, per_block);
+  return g > cap ? cap : g;
 }
 
-template <int NS>
-static int occupancy_ns(bool lds, size_t shmem) {
-  int n = 0;
-  const hipError_t e = lds ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<NS, true, false>, kBlock, shmem)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<NS, false, false>, kBlock, shmem);
-  return (e == hipSuccess && n > 0) ? n : 1;
+hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc, int fd_acc,
+                       int32_t nsegs, int64_t limit, const int64_t* bucket_base, uint32_t* hist,
+                       unsigned long long* seg_distinct, int64_t* bstar, int64_t* rank, unsigned long long* bitmap,
+                       int64_t* dstar, unsigned long long* limit_reached, hipStream_t st) {
+  const unsigned g = grid_cap(cap, kBlock, 8192);
+  hipLaunchKernelGGL(trim_count_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw_seg, acc, fd_acc, bucket_base, hist,
+                     seg_distinct);
+  hipLaunchKernelGGL(trim_select_kernel, dim3((unsigned)nsegs), dim3(256), 0, st, limit, bucket_base, hist,
+                     seg_distinct, bstar, rank, limit_reached);
+  hipLaunchKernelGGL(trim_bitmap_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw_seg, acc, fd_acc, bstar, bitmap);
+  hipLaunchKernelGGL(trim_cutoff_kernel, dim3(grid_for(nsegs, kBlock)), dim3(kBlock), 0, st, nsegs, bstar, rank, bitmap,
+                     dstar);
+  return hipGetLastError();
 }
 
-int scan_blocks_per_cu(int nslots, bool lds, size_t shmem) {
-  switch (ns_for(nslots)) {
-    case 1: return occupancy_ns<1>(lds, shmem);
-    case 2: return occupancy_ns<2>(lds, shmem);
-    case 4: return occupancy_ns<4>(lds, shmem);
-    default: return occupancy_ns<8>(lds, shmem);
-  }
+hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int nw, int has_seg, const uint64_t* sacc,
+                             unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q, int fd_acc,
+                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st) {
+  hipLaunchKernelGGL(hash_merge_kernel, dim3(grid_cap(scap, kBlock, 8192)), dim3(kBlock), 0, st, skeys, scap, nw, has_seg,
+                     sacc, fkeys, fcap, facc, q, fd_acc, dstar, overflow);
+  return hipGetLastError();
 }
 
-hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, hipStream_t st) {
-  const int64_t n = (int64_t)q.nacc * q.num_keys;
-  unsigned g = grid_for(n, kBlock);
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(init_acc_kernel, dim3(g), dim3(kBlock), 0, st, d_acc, q.num_keys, q);
+hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st) {
+  const int64_t nw = (n + 63) / 64;
+  hipLaunchKernelGGL(presence_bitset_kernel, dim3(grid_cap(nw * 64, kBlock, 8192)), dim3(kBlock), 0, st, count, n, bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
+                                int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
+                                hipStream_t st) {
+  if (ngroups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_groups_kernel, dim3(grid_cap(ngroups, kBlock, 8192)), dim3(kBlock), 0, st, slots, ngroups,
+                     keys, nw, cap, acc, nacc, out_keys, out_acc);
   return hipGetLastError();
 }
 

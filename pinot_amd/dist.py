@@ -18,8 +18,9 @@ import hashlib
 import os
 from typing import List, Sequence
 
-OP_SUM_I64, OP_SUM_F64, OP_MIN, OP_MAX = 0, 1, 2, 3
+OP_SUM_I64, OP_SUM_F64, OP_MIN, OP_MAX, OP_SUM_I128, OP_HI = 0, 1, 2, 3, 4, 5
 SIGN = -(1 << 63)  # 0x8000000000000000 as int64
+MASK32 = 0xFFFFFFFF
 
 
 def init_distributed():
@@ -43,25 +44,67 @@ def shard(items: Sequence, rank: int, world: int) -> list:
     return [x for i, x in enumerate(items) if i % world == rank]
 
 
+def _limbs(lo, hi):
+    """A 128-bit two's-complement (hi:lo) as four 32-bit limbs in int64 (the top one signed): summing
+    them across up to 2^31 ranks cannot overflow, so an int64 all-reduce carries the exact sum."""
+    import torch
+    l0 = lo & MASK32
+    l1 = (lo >> 32) & MASK32
+    l2 = hi & MASK32
+    l3 = hi >> 32
+    return torch.stack([l0, l1, l2, l3])
+
+
+def _from_limbs(l):
+    """Carry-propagate summed limbs back into (lo, hi) int64 words."""
+    c = l[0] >> 32
+    w0 = l[0] & MASK32
+    v1 = l[1] + c
+    w1 = v1 & MASK32
+    v2 = l[2] + (v1 >> 32)
+    w2 = v2 & MASK32
+    v3 = l[3] + (v2 >> 32)
+    lo = w0 | (w1 << 32)
+    hi = w2 | (v3 << 32)
+    return lo, hi
+
+
 def merge_tables(table, ops: Sequence[int], num_keys: int, group=None) -> None:
     """In-place all-reduce of a [len(ops), num_keys] int64 tensor of accumulator words.
 
     ops per row: 0 = int64 sum, 1 = fp64 sum (words are double bits), 2/3 = min/max of the
-    library's ordered-uint64 encoding (flipping the sign bit makes it an order-preserving int64)."""
+    library's ordered-uint64 encoding (flipping the sign bit makes it an order-preserving int64),
+    4/5 = low/high word of an exact 128-bit integer sum (all-reduced as 32-bit limbs).
+    One collective per reduction kind: all integer sums (int64 rows and the limbs of 128-bit rows) in
+    one int64 SUM, double sums in one fp64 SUM, and one MIN / one MAX."""
     import torch
     import torch.distributed as dist
     t = table.view(len(ops), num_keys)
-    for i, op in enumerate(ops):
-        row = t[i]
-        if op == OP_SUM_I64:
-            dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
-        elif op == OP_SUM_F64:
-            f = row.view(torch.float64)
-            dist.all_reduce(f, op=dist.ReduceOp.SUM, group=group)
-        else:
-            s = row ^ SIGN
-            dist.all_reduce(s, op=dist.ReduceOp.MIN if op == OP_MIN else dist.ReduceOp.MAX, group=group)
-            row.copy_(s ^ SIGN)
+    ops = list(ops)
+    i64 = [i for i, op in enumerate(ops) if op == OP_SUM_I64]
+    i128 = [i for i, op in enumerate(ops) if op == OP_SUM_I128]
+    f64 = [i for i, op in enumerate(ops) if op == OP_SUM_F64]
+    parts = [t[i64]] if i64 else []
+    parts += [_limbs(t[i], t[i + 1]) for i in i128]
+    if parts:
+        buf = torch.cat(parts).contiguous()
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        if i64:
+            t[i64] = buf[:len(i64)]
+        for j, i in enumerate(i128):
+            lo, hi = _from_limbs(buf[len(i64) + 4 * j: len(i64) + 4 * j + 4])
+            t[i] = lo
+            t[i + 1] = hi
+    if f64:
+        f = t[f64].contiguous().view(torch.float64)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM, group=group)
+        t[f64] = f.view(torch.int64)
+    for op, rop in ((OP_MIN, dist.ReduceOp.MIN), (OP_MAX, dist.ReduceOp.MAX)):
+        rows = [i for i, o in enumerate(ops) if o == op]
+        if rows:
+            s_ = (t[rows] ^ SIGN).contiguous()
+            dist.all_reduce(s_, op=rop, group=group)
+            t[rows] = s_ ^ SIGN
 
 
 _hip = None

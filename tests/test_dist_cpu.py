@@ -107,3 +107,75 @@ def test_shard_is_a_partition():
     parts = [shard(items, r, 8) for r in range(8)]
     assert sorted(sum(parts, [])) == items
     assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+# ------------------------------------------------------------------- exact 128-bit sums across ranks
+I128_RANKS = 8
+I128_KEYS = 365
+
+
+def _rank_sums(rank):
+    """Per-rank exact SUM(impressions)-scale partial sums (~1.3e18 per key and rank: 2.46M docs of
+    values below 2^40 each), so the 8-rank total passes INT64_MAX."""
+    rng = np.random.default_rng(1000 + rank)
+    return [int(x) for x in rng.integers(1 << 60, (1 << 60) + (1 << 58), I128_KEYS, dtype=np.int64)] + \
+           [-(1 << 62) - rank, (1 << 63) - 1 - rank]
+
+
+def _to_words(vals):
+    lo = np.array([v & ((1 << 64) - 1) for v in vals], dtype=np.uint64).view(np.int64)
+    hi = np.array([(v >> 64) & ((1 << 64) - 1) for v in vals], dtype=np.uint64).view(np.int64)
+    return lo, hi
+
+
+def _from_words(lo, hi):
+    out = []
+    for a, b in zip(lo.view(np.uint64), hi.view(np.uint64)):
+        v = (int(b) << 64) | int(a)
+        out.append(v - (1 << 128) if v >> 127 else v)
+    return out
+
+
+def _i128_worker(rank, world, port, out):
+    from pinot_amd import dist as pdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    vals = _rank_sums(rank)
+    lo, hi = _to_words(vals)
+    cnt = np.full(len(vals), 1000 + rank, dtype=np.int64)
+    table = torch.from_numpy(np.concatenate([cnt, lo, hi]).copy())
+    pdist.merge_tables(table, [pdist.OP_SUM_I64, pdist.OP_SUM_I128, pdist.OP_HI], len(vals))
+    if rank == 0:
+        out.put(table.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_int128_sums_merge_exactly_across_8_ranks():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_i128_worker, args=(r, I128_RANKS, port, q)) for r in range(I128_RANKS)]
+    for p in procs:
+        p.start()
+    merged = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = I128_KEYS + 2
+    exp = [sum(_rank_sums(r)[k] for r in range(I128_RANKS)) for k in range(n)]
+    assert max(exp) > (1 << 63)  # past INT64_MAX: an int64 all-reduce would wrap
+    got = _from_words(merged[n:2 * n], merged[2 * n:3 * n])
+    assert got == exp
+    assert list(merged[:n]) == [sum(1000 + r for r in range(I128_RANKS))] * n
+
+
+def test_int128_limbs_round_trip():
+    from pinot_amd.dist import _from_limbs, _limbs
+    vals = [0, 1, -1, (1 << 63) - 1, -(1 << 63), (1 << 100) + 12345, -(1 << 120) - 7, (1 << 126)]
+    lo, hi = _to_words(vals)
+    l = _limbs(torch.from_numpy(lo), torch.from_numpy(hi))
+    a, b = _from_limbs(l)
+    assert _from_words(a.numpy(), b.numpy()) == vals

@@ -42,7 +42,6 @@ HC_QUERIES = [
 @pytest.mark.parametrize("qi", range(len(HC_QUERIES)))
 @pytest.mark.parametrize("n", [1, 5000, 300_007])
 def test_highcard_partitioned_vs_oracle(engine, qi, n, monkeypatch):
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
     rng = np.random.default_rng(1000 + qi * 7 + n)
     bufs = random_segment(rng, n, bits_cards=(1000, 1000))
@@ -73,7 +72,6 @@ def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch, stage_cap,
     segs = [engine.ImmutableSegment(b) for b in bufs]
     q = ("SET numGroupsLimit = 2000000; SELECT d0, d1, COUNT(*), SUM(r_int), SUM(r_long), MIN(r_double), "
          "MAX(r_long) FROM t WHERE r_long > -100000000000 GROUP BY d0, d1")
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     monkeypatch.setenv("PINOT_AMD_PARTITIONED", "1")
     rp = engine.ServerQueryExecutor().execute(q, segs)
     assert rp.kernel_info() == "jit-partitioned"
@@ -93,7 +91,6 @@ def test_highcard_partitioned_equals_atomic_plan(engine, monkeypatch, stage_cap,
 def test_highcard_multi_segment_merged_dictionaries(engine, monkeypatch):
     """Segments with different dictionaries: keys remapped into the merged key space, then
     partitioned; dictionary-encoded FLOAT/DOUBLE metric columns feed the records."""
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     rng = np.random.default_rng(5)
     bufs = []
     for i in range(4):
@@ -116,7 +113,6 @@ def test_highcard_multi_segment_merged_dictionaries(engine, monkeypatch):
 
 
 def test_num_groups_limit_reached_flag(engine, monkeypatch):
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     rng = np.random.default_rng(9)
     bufs = random_segment(rng, 50_000, bits_cards=(1000, 1000))
     seg = engine.ImmutableSegment(bufs)
@@ -132,10 +128,9 @@ def test_num_groups_limit_reached_flag(engine, monkeypatch):
 def test_wide_lds_table_plan(engine, monkeypatch, wide):
     """A group table between 40 KiB and the 160 KiB workgroup LDS runs in one CU-wide block per CU
     (PINOT_AMD_WIDE_LDS=0: the partitioned plan instead); both equal the oracle."""
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     monkeypatch.setenv("PINOT_AMD_WIDE_LDS", wide)
     rng = np.random.default_rng(21)
-    bufs = [random_segment(rng, 250_000 + 17 * i, name=f"w{i}", bits_cards=(1000, 5)) for i in range(2)]
+    bufs = [random_segment(rng, 250_000 + 17 * i, name=f"w{i}", bits_cards=(1000, 4)) for i in range(2)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
     q = ("SELECT d0, d1, COUNT(*), SUM(r_long), MAX(r_double), MIN(r_int) FROM t WHERE r_int > -500000 "
          "GROUP BY d0, d1 OPTION(numGroupsLimit=1000000)")
@@ -153,7 +148,6 @@ def test_highcard_sampled_handover(engine, monkeypatch, where, stride):
     stride-th tile; an extrapolated count under docs/64 skips the count pass and leaves the batch to
     the direct-atomic scan. Selective (0.25%), broad (50%) and docId-clustered (sorted `ts`) filters,
     sampling off ("0") and a non-power-of-two stride: identical groups and matched-doc count."""
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
     monkeypatch.delenv("PINOT_AMD_ATOMIC_HANDOVER", raising=False)
     if stride is None:

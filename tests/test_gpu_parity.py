@@ -38,16 +38,23 @@ def _inverted_index_always(monkeypatch):
     monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
 
 
-@pytest.fixture(params=["jit", "aot"])
+@pytest.fixture(params=["auto", "hash"])
 def kernel_mode(request, monkeypatch):
-    """Run a test through the hipRTC query-specialised kernel and through the AOT generic kernel."""
-    monkeypatch.setenv("PINOT_AMD_JIT", "1" if request.param == "jit" else "0")
+    """Run a test through the planner's own choice (dense LDS / CU-wide / partitioned tables) and
+    through the hash-table GROUP BY plan forced on every grouped query (the plan that serves key spaces
+    past the dense table and numGroupsLimit trimming), both against the same oracle."""
+    if request.param == "hash":
+        monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    else:
+        monkeypatch.delenv("PINOT_AMD_GROUP_PLAN", raising=False)
     return request.param
 
 
 def check_mode(res, mode):
     info = res.kernel_info()
-    assert info.startswith(mode), info
+    assert info.startswith("jit"), info
+    if mode == "hash" and res.qc.group_by:
+        assert "hash" in info, info
 
 
 @pytest.fixture(scope="module")
@@ -90,13 +97,15 @@ def test_golden_inner_aggregation(engine, sv, with_filter, use_inverted, kernel_
     assert_same_groups(res.groups(), og)
 
 
-@pytest.mark.parametrize("case", [c for c in EXP["inner_group_by"]["cases"] if len(c["group_by"]) <= 3],
+@pytest.mark.parametrize("case", EXP["inner_group_by"]["cases"],
                          ids=lambda c: f"{len(c['group_by'])}cols-f{int(c['filter'])}")
 def test_golden_inner_group_by(engine, sv, case, kernel_mode):
     bufs, seg = sv
     q = INNER_QUERY + (SV_FILTER if case["filter"] else "") + " GROUP BY " + ", ".join(case["group_by"])
     res = engine.ServerQueryExecutor().execute(q, [seg])
     check_mode(res, kernel_mode)
+    if len(case["group_by"]) >= 5:  # key spaces of 2^43+ (5 columns) and 2^80 (9 columns): hash table
+        assert "hash" in res.kernel_info()
     groups = res.groups()
     cnt, s1, mx3, mn6, avg7 = groups[tuple(case["key"])]
     assert [cnt, s1, mx3, mn6, avg7[0], avg7[1]] == case["values"]
@@ -285,10 +294,20 @@ def test_errors_are_loud(engine):
     with pytest.raises(PinotAmdError):
         engine.ServerQueryExecutor().execute("SELECT nope, COUNT(*) FROM t GROUP BY nope", [seg])
     with pytest.raises(PinotAmdError):
-        # three raw keys of ~1000 distinct values each x a 143-value dictionary key: a key space past
-        # the dense table (2^28 keys)
-        engine.ServerQueryExecutor().execute("SELECT r_int, r_long, r_double, d1, COUNT(*) FROM t "
-                                             "GROUP BY r_int, r_long, r_double, d1", [seg])
+        engine.ServerQueryExecutor().execute("SELECT SUMLONG(r_double) FROM t", [seg])
+
+
+def test_key_space_past_the_dense_table(engine):
+    """Three raw keys of ~1000 distinct values each x a 143-value dictionary key (1.4e11 keys; this
+    shape once aborted a dense-table plan): served by the hash-table plan, equal to the oracle."""
+    rng = np.random.default_rng(2)
+    bufs = random_segment(rng, 1000)
+    seg = engine.ImmutableSegment(bufs)
+    q = "SELECT r_int, r_long, r_double, d1, COUNT(*), SUM(r_long) FROM t GROUP BY r_int, r_long, r_double, d1"
+    res = engine.ServerQueryExecutor().execute(q, [seg])
+    assert "hash" in res.kernel_info()
+    _, og = oracle.execute(q, [bufs])
+    assert_same_groups(res.groups(), og)
 
 
 FILTERS = [

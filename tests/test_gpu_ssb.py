@@ -32,7 +32,6 @@ def flat(request, engine):
 
 @pytest.mark.parametrize("qi", range(len(EXP["queries"])), ids=[q["name"] for q in EXP["queries"]])
 def test_ssb_golden(engine, flat, qi, monkeypatch):
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     bufs, segs = flat
     q = EXP["queries"][qi]
     res = engine.ServerQueryExecutor().execute(q["sql"], segs)
@@ -48,31 +47,24 @@ def test_ssb_golden(engine, flat, qi, monkeypatch):
     assert got == {k: v[0] for k, v in og.items()} or not q["group_by"]
 
 
-@pytest.mark.parametrize("name", ["Q1.1", "Q4.1"])
-def test_ssb_expressions_need_jit(engine, flat, name, monkeypatch):
-    """The generic AOT kernel reads plain columns only: an expression aggregation fails loudly."""
-    from pinot_amd._lib import PinotAmdError
-    monkeypatch.setenv("PINOT_AMD_JIT", "0")
-    _, segs = flat
-    sql = dict(ssb.SSB_QUERIES)[name]
-    with pytest.raises(PinotAmdError):
-        engine.ServerQueryExecutor().execute(sql, segs)
-
-
-@pytest.mark.parametrize("name", ["Q2.1", "Q3.1", "Q3.3"])
-def test_ssb_plain_sums_through_aot(engine, flat, name, monkeypatch):
-    monkeypatch.setenv("PINOT_AMD_JIT", "0")
+@pytest.mark.parametrize("name", ["Q1.1", "Q2.1", "Q3.1", "Q3.3", "Q4.1"])
+def test_ssb_through_hash_plan(engine, flat, name, monkeypatch):
+    """The same queries through the hash-table GROUP BY plan (forced), against the oracle."""
+    monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
     bufs, segs = flat
     sql = dict(ssb.SSB_QUERIES)[name]
     res = engine.ServerQueryExecutor().execute(sql, segs)
-    assert res.kernel_info().startswith("aot")
-    _, og = oracle.execute(sql, bufs)
-    assert res.groups() == og
+    if parse_sql(sql).group_by:
+        assert "hash" in res.kernel_info()
+    nm, og = oracle.execute(sql, bufs)
+    got = res.groups()
+    if not parse_sql(sql).group_by and nm == 0:
+        og = {(): og[()]}
+    assert got == og
 
 
 def test_ssb_synthetic_segment_vs_oracle(engine, monkeypatch):
     """The SF-scaled generator's segments (bench input) through every query, against the oracle."""
-    monkeypatch.setenv("PINOT_AMD_JIT", "1")
     bufs = [ssb.lineorder_flat_segment(f"lf{i}", 150_001 + i, seed=i) for i in range(2)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
     for name, sql in ssb.SSB_QUERIES:
