@@ -80,22 +80,6 @@ def cpu_baseline(workload: str, query: str, seg_rows: int, seconds: float, threa
                       f"path), {wall:.1f} s wall"}
 
 
-def query_bytes_per_row(query: str, seg) -> float:
-    """Algorithmic HBM bytes per row: every column the query references, read once (fixed-bit
-    columns at their bit width, raw columns at their value width)."""
-    from pinot_amd.query import parse_sql
-    from pinot_amd.segment import VALUE_SIZE
-    qc = parse_sql(query)
-    cols = set(qc.group_by) | {c for a in qc.aggregations for c in a.columns}
-    for clause in qc.cnf:
-        cols |= {p.column for p, _ in clause}
-    total = 0.0
-    for c in cols:
-        cb = seg.columns[c]
-        total += cb.bits_per_element / 8.0 if cb.has_dictionary else VALUE_SIZE[cb.stored_type]
-    return total
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,6 +96,19 @@ def main():
     ap.add_argument("--query-index", type=int, default=None, help="run only this query of the workload")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not under a launcher: start one rank per GPU as child processes (torchrun) before anything
+        # touches the GPU, and exit with the launcher's status
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        log(f"spawning {args.gpus} ranks: {' '.join(cmd)}")
+        import subprocess
+        sys.exit(subprocess.call(cmd))
+
     import torch
     import torch.distributed as dist
     from pinot_amd import dist as pdist, engine
@@ -123,9 +120,17 @@ def main():
         args.segments = 60 if args.workload == "ssb" else 100
 
     rank, world, local = pdist.init_distributed()
-    torch.cuda.set_device(local)
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE {world}")
+        sys.exit(2)
+    torch.cuda.set_device(local)
+    if world > 1:
+        if dist.get_world_size() != args.gpus:
+            log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+            sys.exit(2)
+        if local >= torch.cuda.device_count():
+            log(f"error: local rank {local} but only {torch.cuda.device_count()} visible GPUs")
+            sys.exit(2)
 
     # ---- stage this rank's segments into HBM ----
     t0 = time.time()
@@ -139,8 +144,6 @@ def main():
         else:  # slow-to-build workloads: further segments are HBM copies of the first `distinct`
             bufs = host_bufs[i % distinct]
         segs.append(engine.ImmutableSegment(bufs))
-        if i == 0:
-            first_bufs = bufs
         if i % 20 == 19:
             log(f"[rank {rank}] staged {i + 1}/{args.segments} segments ({time.time() - t0:.0f}s)")
     hbm = sum(s.device_bytes() for s in segs)
@@ -154,8 +157,21 @@ def main():
     rows_per_rank = args.segments * args.rows
     outs = []
     for query in queries:
-        bpr = bytes_per_row if bytes_per_row is not None else query_bytes_per_row(query, first_bufs)
+        # cold query latency: host planning + predicate resolution + hipRTC compile (first time this
+        # shape is seen in the process) + first launch + result fetch; then the same with the
+        # compiled kernel cached (a repeated query shape on a server)
+        torch.cuda.synchronize()
+        t_c = time.perf_counter()
         res = ex.execute(query, segs, stream=stream)
+        res.groups()
+        torch.cuda.synchronize()
+        cold_ms = (time.perf_counter() - t_c) * 1e3
+        t_c = time.perf_counter()
+        res2 = ex.execute(query, segs, stream=stream)
+        res2.groups()
+        torch.cuda.synchronize()
+        plan_ms = (time.perf_counter() - t_c) * 1e3
+        res2.destroy()
         scratch = None
 
         def step():
@@ -188,7 +204,13 @@ def main():
         total_rows = rows_per_rank * world * args.steps
         value = total_rows / elapsed
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        alg_bytes = rows_per_rank * bpr   # per launch (one launch = all segments)
+        # algorithmic bytes per execution, from the plan (pinot_amd_result_algorithmic_bytes): each
+        # decoded column once at its stored width; under an inverted-index gate only the rows that
+        # pass it, plus the selected bitmaps and the dense bitset written + read once
+        alg_bytes = res.algorithmic_bytes()
+        if bytes_per_row is not None:
+            assert abs(alg_bytes - rows_per_rank * bytes_per_row) <= 1e-6 * alg_bytes, (alg_bytes, bytes_per_row)
+        bpr = alg_bytes / rows_per_rank
         achieved = alg_bytes / avg_kernel_s / 1e9
 
         groups = res.groups()
@@ -264,6 +286,8 @@ def main():
                     "hbm_bytes_per_gpu": hbm,
                     "scan_kernel": res.kernel_info(),
                 },
+                "cold_ms": cold_ms,
+                "cached_plan_ms": plan_ms,
                 "roofline": {
                     "bound": "hbm",
                     "achieved": achieved,

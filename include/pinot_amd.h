@@ -245,6 +245,11 @@ int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int
 /* Which scan kernel the plan runs: "jit" (query-specialised, compiled with hipRTC) or
  * "aot: <reason>" (the generic precompiled kernel). */
 const char* pinot_amd_result_kernel_info(pinot_amd_result* r);
+/* Algorithmic HBM bytes of the last execution (the roofline numerator): every decoded column once
+ * (fixed-bit columns at their bit width, raw columns at their value width); under an inverted-index
+ * gate only the rows that pass it; plus, per inverted-index leaf, the selected bitmaps' serialized
+ * bytes and the dense docId bitset written and read once. */
+int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes);
 /* Kernel timing of the last execute: device milliseconds of the fused scan kernel, measured with
  * HIP events on the execution stream. */
 int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms);

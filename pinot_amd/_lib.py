@@ -92,6 +92,7 @@ SIGNATURES = {
     "pinot_amd_result_accumulators": (C.c_int, [_P, C.POINTER(C.c_int32), _I64P, _PP, C.POINTER(C.c_int32)]),
     "pinot_amd_result_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "pinot_amd_result_kernel_info": (C.c_char_p, [_P]),
+    "pinot_amd_result_algorithmic_bytes": (C.c_int, [_P, C.POINTER(C.c_double)]),
 }
 
 _lib = None

@@ -735,6 +735,8 @@ struct Launch {
   size_t shmem = 0, shmem_scatter = 0, shmem_agg = 0;
   DevPartition part{};
   int64_t docs = 0, tiles = 0;
+  double col_bytes = 0;  // algorithmic bytes of the launch's decoded columns over all its docs
+  bool gated = false;    // an inverted-index gate clause: columns are read only where it passes
 };
 
 enum PlanKind { PLAN_DENSE = 0, PLAN_PARTITIONED = 1, PLAN_HASH = 2, PLAN_FILTER = 3 };
@@ -754,6 +756,7 @@ struct pinot_amd_result {
     DevBuf* grp;   // chunk k's containers: sel[grp[k] .. grp[k+1])
     int32_t nsel, nchunks;
     int64_t num_docs;
+    double alg_bytes;  // selected bitmap payloads + the dense bitset written and read once
   };
   std::vector<InvLeaf> inv_leaves;
   DevBuf d_expand_jobs;        // one ExpandJob per inv_leaves entry (batched clear + expand launches)
@@ -1061,7 +1064,10 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     auto gb = std::make_unique<DevBuf>();
     rc = gb->alloc_copy(grp.data(), grp.size() * 4, 64);
     if (rc) return rc;
-    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), nchunks, seg->num_docs});
+    double sel_bytes = 0;
+    for (int32_t d : ids) sel_bytes += (double)(c.inv_bytes[d + 1] - c.inv_bytes[d]);
+    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), nchunks, seg->num_docs,
+                             sel_bytes + 2.0 * (double)((seg->num_docs + 7) / 8)});
     r->owned.push_back(std::move(gb));
     L->kind = LEAF_DOC_BITSET;
     L->bits = (const uint32_t*)bs->p;
@@ -1863,6 +1869,20 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.stage_cap = cap >= 4 ? cap : 0;
       if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
     }
+    {  // algorithmic bytes: each decoded column once (fixed-bit at its width, raw at its value width)
+      for (size_t k = 0; k < L.segs.size(); ++k)
+        for (int sl = 0; sl < nslots; ++sl) {
+          const DevColumn& dc = ls[k].cols[sl];
+          const double bpr = dc.enc == ENC_FIXED_BIT ? dc.bits / 8.0 : dc.enc == ENC_RAW ? (double)value_size(dc.type) : 0.0;
+          L.col_bytes += bpr * (double)ls[k].num_docs;
+        }
+      std::vector<int> gate(nclauses, 1), has(nclauses, 0);
+      for (const JitLeaf& jl : jp.leaves) {
+        has[jl.clause] = 1;
+        if (jl.kinds != (1u << LEAF_DOC_BITSET) || jl.negate) gate[jl.clause] = 0;
+      }
+      for (int c = 0; c < nclauses; ++c) L.gated |= gate[c] && has[c];
+    }
     L.jit = jit_get(jp, &r->jit_status);
     if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
@@ -2058,6 +2078,25 @@ int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   int64_t total = 0;
   for (size_t li = 0; li < r->launches.size(); ++li) total += (int64_t)std::max(c[3 * li], c[3 * li + 2]);
   *h_out = total;
+  return 0;
+}
+
+int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes) {
+  if (!r || !h_bytes) return fail(PINOT_AMD_EINVAL, "algorithmic_bytes: bad arguments");
+  std::vector<unsigned long long> c;
+  if (int rc = read_counters(r, &c)) return rc;
+  double b = 0;
+  for (const auto& il : r->inv_leaves) b += il.alg_bytes;
+  for (size_t li = 0; li < r->launches.size(); ++li) {
+    const Launch& L = r->launches[li];
+    if (!L.gated || L.docs == 0) {
+      b += L.col_bytes;
+    } else {  // gated: only the rows that pass the filter need their column bytes
+      const double m = (double)std::max(c[3 * li], c[3 * li + 2]);
+      b += L.col_bytes * m / (double)L.docs;
+    }
+  }
+  *h_bytes = b;
   return 0;
 }
 

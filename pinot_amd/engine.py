@@ -211,6 +211,12 @@ class QueryResult:
         check(lib().pinot_amd_result_last_kernel_ms(self._h, C.byref(out)), "last_kernel_ms")
         return out.value
 
+    def algorithmic_bytes(self) -> float:
+        """Algorithmic HBM bytes of the last execution (pinot_amd_result_algorithmic_bytes)."""
+        out = C.c_double()
+        check(lib().pinot_amd_result_algorithmic_bytes(self._h, C.byref(out)), "algorithmic_bytes")
+        return out.value
+
     def accumulators(self):
         """(ops, num_keys, [device pointers]) of the dense accumulators for a cross-GPU merge."""
         n = C.c_int32()
