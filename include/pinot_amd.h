@@ -56,7 +56,10 @@ enum pinot_amd_predicate_type { PINOT_AMD_EQ = 0, PINOT_AMD_NOT_EQ = 1, PINOT_AM
 
 /* Aggregation functions (pinot-segment-spi/.../AggregationFunctionType.java) */
 enum pinot_amd_agg_type { PINOT_AMD_AGG_COUNT = 0, PINOT_AMD_AGG_SUM = 1, PINOT_AMD_AGG_MIN = 2,
-                          PINOT_AMD_AGG_MAX = 3, PINOT_AMD_AGG_SUMLONG = 4, PINOT_AMD_AGG_AVG = 5 };
+                          PINOT_AMD_AGG_MAX = 3, PINOT_AMD_AGG_SUMLONG = 4, PINOT_AMD_AGG_AVG = 5,
+                          /* MinMaxRangeAggregationFunction: (min, max) pair built with < / > (NaN never
+                           * enters it); final result max - min */
+                          PINOT_AMD_AGG_MINMAXRANGE = 6 };
 
 /* ------------------------------------------------------------------------------------------------
  * Runtime
@@ -193,6 +196,14 @@ enum pinot_amd_expr_op { PINOT_AMD_EXPR_COLUMN = 0, PINOT_AMD_EXPR_MUL = 1, PINO
                          PINOT_AMD_EXPR_ADD = 3 };
 int pinot_amd_query_add_aggregation_expr(pinot_amd_query* q, int32_t agg_type, int32_t expr_op, const char* column_a,
                                          const char* column_b, int32_t* out_index);
+/* Install the group key space of group-by column `column` (values in the column's stored type, any
+ * order; duplicates ignored): the union of the dictionaries of every server's segments, so that the
+ * dense accumulator tables of all servers index groups identically and can be merged in place
+ * (the broker merges by value: GroupByDataTableReducer.java:258). Must hold every dictionary value of
+ * the segments executed (EINVAL otherwise). Without it the key space is the union over the batch. */
+int pinot_amd_query_set_group_key_values(pinot_amd_query* q, const char* column, int32_t stored_type, int64_t n,
+                                         const int64_t* h_values_i, const double* h_values_d,
+                                         const char* const* h_values_s);
 /* QueryOptions numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000). */
 int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit);
 
@@ -235,6 +246,11 @@ int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_ou
  * integer columns / SUMLONG. Groups are ordered by ascending global key. */
 int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, double* h_values,
                            int64_t* h_values_i64, int64_t* h_num_fetched);
+/* AggregationFunction.extractAggregationResult: the intermediate result of every aggregation, two
+ * doubles per (group, aggregation) in fetch order — AVG: AvgPair (sum, count); MINMAXRANGE:
+ * MinMaxRangePair (min, max); every other function: (final value, 0). What a server hands the broker
+ * for the cross-server merge. */
+int pinot_amd_result_fetch_intermediate(pinot_amd_result* r, int64_t cap, double* h_pairs, int64_t* h_num_fetched);
 /* String value of merged-dictionary id `id` for group-by column j. */
 const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t id);
 /* Device view of the dense accumulators for a multi-GPU merge (RCCL all-reduce in place):

@@ -20,7 +20,7 @@ from typing import Dict, List, Sequence
 
 import numpy as np
 
-from pinot_amd.query import (QueryContext, fold_distinct_count, merge_partial, parse_sql, reduce_rows,
+from pinot_amd.query import (JavaDouble, QueryContext, canonical_key, distinct_value, merge_partial, parse_sql, reduce_rows,
                              split_distinct_count)
 from pinot_amd.segment import (DOUBLE, FLOAT, INT, LONG, STRING, ColumnBuffers, SegmentBuffers,
                                parse_raw_fwd_header)
@@ -31,7 +31,7 @@ LIB = os.path.join(HERE, "libpinot_oracle.so")
 OR_TYPE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3}
 OR_ENC = {"FIXED_BIT": 0, "RAW": 1, "SORTED": 2}
 DICT_RANGE, DICT_SET, RAW_RANGE, RAW_IN, DOC_BITSET = 0, 1, 2, 3, 4
-AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4}
+AGG = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4, "RMIN": 5, "RMAX": 6}
 
 
 class OColumn(C.Structure):
@@ -343,12 +343,25 @@ class OracleSegment:
             self._raw_groups[g] = (i, dvals)
         return self._raw_groups[g][0]
 
+    def values(self, col: str) -> np.ndarray:
+        """Every doc's value of a column: dictionary values through the forward index's dictIds
+        (FixedBitSVForwardIndexReaderV2 / SortedIndexReaderImpl + Dictionary.get), raw values decoded."""
+        cb = self.seg.columns[col]
+        n = self.seg.num_docs
+        if cb.encoding == "RAW":
+            return np.frombuffer(raw_values_region(cb).tobytes(), dtype=np.dtype(
+                {INT: ">i4", LONG: ">i8", FLOAT: ">f4", DOUBLE: ">f8"}[cb.stored_type]), count=n)
+        ids = np.zeros(max(n, 1), dtype=np.int32)
+        lib().oracle_column_dict_ids(C.byref(self.cols[self.index[col]]), 0, n, _ptr(ids))
+        dv = cb.dict_values if cb.stored_type != STRING else np.asarray(cb.dict_values, dtype=object)
+        return dv[ids[:n]]
+
     def key_values(self, dict_ids, group_by: Sequence[str]) -> tuple:
         out = []
         for g, d in zip(group_by, dict_ids):
             cb = self.seg.columns[g]
             v = self._raw_groups[g][1][int(d)] if g in self._raw_groups else cb.dict_values[int(d)]
-            out.append(v if cb.stored_type == STRING else (float(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
+            out.append(v if cb.stored_type == STRING else (JavaDouble(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
         return tuple(out)
 
 
@@ -358,10 +371,8 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
     segments with AggregationFunction.merge semantics (GroupByCombineOperator's upsert by key).
     stats, when given, receives 'num_groups_limit_reached' (any segment's GroupByOperator flag)."""
     qc = parse_sql(query) if isinstance(query, str) else query
-    if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):  # per-group value sets (query.py)
-        base, subs = split_distinct_count(qc)
-        total, bg = execute(base, segments, use_inverted, stats)
-        return total, fold_distinct_count(qc, bg, [(i, execute(sq, segments, use_inverted)[1]) for i, sq in subs])
+    if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):
+        return _distinct_count(qc, segments, use_inverted, stats)
     if stats is not None:
         stats["num_groups_limit_reached"] = False
     total = 0
@@ -382,8 +393,8 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
                 nat.append(("COUNT", "*", None))
                 slots.append(("avg", len(nat) - 2, len(nat) - 1))
             elif a.func == "MINMAXRANGE":  # MinMaxRangeAggregationFunction: MinMaxRangePair(min, max)
-                nat.append(("MIN", a.column, a.expr))
-                nat.append(("MAX", a.column, a.expr))
+                nat.append(("RMIN", a.column, a.expr))
+                nat.append(("RMAX", a.column, a.expr))
                 slots.append(("range", len(nat) - 2, len(nat) - 1))
             else:
                 nat.append((a.func, a.column, a.expr))
@@ -434,6 +445,43 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
         groups[k] = [(float(p[0]), p[1]) if a.func == "AVG" else float(p) if a.func == "SUM" else p
                      for a, p in zip(qc.aggregations, parts)]
     return total, groups
+
+
+def _distinct_count(qc: QueryContext, segments, use_inverted: bool, stats):
+    """DistinctCountAggregationFunction (aggregate / aggregateGroupBySV: add each matching doc's value
+    to its group's set; merge = union; final = size), restated directly over the docs: the filter's
+    matching docs, their group-by values and their DISTINCTCOUNT column values, with value identity
+    as the fastutil sets have it (query.distinct_value). The other aggregations come from the query
+    without its DISTINCTCOUNTs, whose groups are the groups of the query."""
+    base, _ = split_distinct_count(qc)
+    total, bg = execute(base, segments, use_inverted, stats)
+    dc = [i for i, a in enumerate(qc.aggregations) if a.func == "DISTINCTCOUNT"]
+    sets = {i: {} for i in dc}
+    for seg in segments:
+        os_ = OracleSegment(seg)
+        n = seg.num_docs
+        if qc.cnf:
+            bits, _ = os_.filter_bitset(qc, use_inverted)
+            docs = np.flatnonzero(np.unpackbits(bits.view(np.uint8), bitorder="little")[:n])
+        else:
+            docs = np.arange(n)
+        keys = [os_.values(g)[docs].tolist() for g in qc.group_by]
+        for i in dc:
+            vals = os_.values(qc.aggregations[i].column)[docs].tolist()
+            s = sets[i]
+            for d in range(len(docs)):
+                k = canonical_key(tuple(kc[d] for kc in keys))
+                s.setdefault(k, set()).add(distinct_value(vals[d]))
+    rest = [j for j, a in enumerate(qc.aggregations) if a.func != "DISTINCTCOUNT"]
+    out = {}
+    for key, parts in bg.items():
+        full = [None] * len(qc.aggregations)
+        for j, p in zip(rest, parts):
+            full[j] = p
+        for i in dc:
+            full[i] = frozenset(sets[i].get(canonical_key(key), ()))
+        out[key] = full
+    return total, out
 
 
 def _is_int_value(seg: SegmentBuffers, column, expr) -> bool:

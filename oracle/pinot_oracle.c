@@ -492,7 +492,8 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
   int64_t* li = (int64_t*)calloc((size_t)naggs, sizeof(int64_t));
   __int128* exact = (__int128*)calloc((size_t)naggs, sizeof(__int128));
   for (int32_t a = 0; a < naggs; a++) {
-    holder[a] = aggs[a].func == OR_AGG_MIN ? INFINITY : aggs[a].func == OR_AGG_MAX ? -INFINITY : 0.0;
+    const int f = aggs[a].func;
+    holder[a] = (f == OR_AGG_MIN || f == OR_AGG_RMIN) ? INFINITY : (f == OR_AGG_MAX || f == OR_AGG_RMAX) ? -INFINITY : 0.0;
   }
   int64_t doc = 0;
   while (doc < num_docs) {
@@ -543,6 +544,20 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
           holder[a] = (isnan(m) || isnan(holder[a])) ? NAN : fmax(m, holder[a]);
           break;
         }
+        /* MinMaxRangeAggregationFunction.aggregateSV (:95-103): MinMaxRangePair.apply(value) compares
+         * with < / > (MinMaxRangePair.java:37-48), so NaN never enters the pair */
+        case OR_AGG_RMIN:
+          for (int32_t i = 0; i < len; i++) {
+            const double v = agg_f64(cols, &aggs[a], block[i]);
+            if (v < holder[a]) holder[a] = v;
+          }
+          break;
+        case OR_AGG_RMAX:
+          for (int32_t i = 0; i < len; i++) {
+            const double v = agg_f64(cols, &aggs[a], block[i]);
+            if (v > holder[a]) holder[a] = v;
+          }
+          break;
       }
     }
   }
@@ -577,7 +592,7 @@ typedef struct {
 } or_holder;
 
 static void holder_init(or_holder* h, int func) {
-  h->h = func == OR_AGG_MIN ? INFINITY : func == OR_AGG_MAX ? -INFINITY : 0.0;
+  h->h = (func == OR_AGG_MIN || func == OR_AGG_RMIN) ? INFINITY : (func == OR_AGG_MAX || func == OR_AGG_RMAX) ? -INFINITY : 0.0;
   h->li = 0;
   h->exact = 0;
 }
@@ -596,6 +611,11 @@ static void holder_add(or_holder* h, const oracle_column* cols, const oracle_agg
     case OR_AGG_SUMLONG: h->li = (int64_t)((uint64_t)h->li + (uint64_t)value_i64(c, doc)); break;
     case OR_AGG_MIN: { double v = agg_f64(cols, a, doc); if (v < h->h) h->h = v; break; }
     case OR_AGG_MAX: { double v = agg_f64(cols, a, doc); if (v > h->h) h->h = v; break; }
+    /* MinMaxRangeAggregationFunction.setGroupByResult (:105-114): a group's first doc creates the pair
+     * from its value (NaN included, which then stays: every later < / > against NaN is false); later
+     * docs apply with < / >. li marks "pair created". */
+    case OR_AGG_RMIN: { double v = agg_f64(cols, a, doc); if (!h->li || v < h->h) h->h = v; h->li = 1; break; }
+    case OR_AGG_RMAX: { double v = agg_f64(cols, a, doc); if (!h->li || v > h->h) h->h = v; h->li = 1; break; }
   }
 }
 

@@ -34,7 +34,9 @@ enum {
   OR_PRED_DOC_BITSET = 4    /* precomputed docId bitset      BitmapBasedFilterOperator (inverted index) */
 };
 /* aggregation functions */
-enum { OR_AGG_COUNT = 0, OR_AGG_SUM = 1, OR_AGG_MIN = 2, OR_AGG_MAX = 3, OR_AGG_SUMLONG = 4 };
+/* OR_AGG_RMIN / OR_AGG_RMAX: the two sides of MINMAXRANGE's MinMaxRangePair */
+enum { OR_AGG_COUNT = 0, OR_AGG_SUM = 1, OR_AGG_MIN = 2, OR_AGG_MAX = 3, OR_AGG_SUMLONG = 4, OR_AGG_RMIN = 5,
+       OR_AGG_RMAX = 6 };
 
 typedef struct {
   int32_t encoding;      /* OR_ENC_* */

@@ -77,6 +77,8 @@ SIGNATURES = {
     "pinot_amd_query_add_group_by": (C.c_int, [_P, C.c_char_p]),
     "pinot_amd_query_add_aggregation": (C.c_int, [_P, C.c_int32, C.c_char_p, C.POINTER(C.c_int32)]),
     "pinot_amd_query_set_num_groups_limit": (C.c_int, [_P, C.c_int64]),
+    "pinot_amd_query_set_group_key_values": (C.c_int, [_P, C.c_char_p, C.c_int32, C.c_int64, _I64P,
+                                                       C.POINTER(C.c_double), C.POINTER(C.c_char_p)]),
     "pinot_amd_query_add_aggregation_expr": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
                                                        C.POINTER(C.c_int32)]),
     "pinot_amd_result_num_groups_limit_reached": (C.c_int, [_P, C.POINTER(C.c_int32)]),
@@ -88,6 +90,7 @@ SIGNATURES = {
     "pinot_amd_result_num_docs_matched": (C.c_int, [_P, _I64P]),
     "pinot_amd_result_num_groups": (C.c_int, [_P, _I64P]),
     "pinot_amd_result_fetch": (C.c_int, [_P, C.c_int64, _I64P, C.POINTER(C.c_double), _I64P, _I64P]),
+    "pinot_amd_result_fetch_intermediate": (C.c_int, [_P, C.c_int64, C.POINTER(C.c_double), _I64P]),
     "pinot_amd_result_string_key": (C.c_char_p, [_P, C.c_int32, C.c_int64]),
     "pinot_amd_result_accumulators": (C.c_int, [_P, C.POINTER(C.c_int32), _I64P, _PP, C.POINTER(C.c_int32)]),
     "pinot_amd_result_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),

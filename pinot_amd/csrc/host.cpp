@@ -141,6 +141,23 @@ static std::u16string to_utf16(const std::string& s) {
 }
 static bool java_less(const std::string& a, const std::string& b) { return to_utf16(a) < to_utf16(b); }
 
+// Double.compare / Double.doubleToLongBits order: -0.0 < 0.0, every NaN equal and greatest. Group
+// keys of FLOAT/DOUBLE columns are told apart this way (fastutil's Double2IntOpenHashMap compares
+// doubleToLongBits; sorted dictionaries use Double.compare), so merged key columns sort by it.
+static uint64_t java_double_order(double v) {
+  uint64_t b;
+  if (std::isnan(v)) b = 0x7ff8000000000000ull;
+  else memcpy(&b, &v, 8);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+static double java_double_from_order(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  double v;
+  memcpy(&v, &b, 8);
+  return v;
+}
+static bool java_double_less(double a, double b) { return java_double_order(a) < java_double_order(b); }
+
 struct RoaringContainerHost {
   uint32_t key, kind, count, pad;
   uint64_t offset;
@@ -610,9 +627,19 @@ struct AggSpec {
   std::string column2;  // second operand of an expression
 };
 
+struct MergedKeyColumn {
+  int32_t type = 0;
+  std::vector<int64_t> vi;
+  std::vector<double> vd;
+  std::vector<std::string> vs;
+  size_t size() const { return type == T_STRING ? vs.size() : is_float(type) ? vd.size() : vi.size(); }
+};
+
 struct pinot_amd_query {
   std::vector<PredSpec> preds;
   std::vector<std::string> group_by;
+  // group-by column -> key space installed by the caller (the union of every server's dictionaries)
+  std::map<std::string, MergedKeyColumn> key_space;
   std::vector<AggSpec> aggs;
   int64_t num_groups_limit = 100000;
 };
@@ -675,7 +702,7 @@ int pinot_amd_query_add_group_by(pinot_amd_query* q, const char* column) {
 
 int pinot_amd_query_add_aggregation(pinot_amd_query* q, int32_t agg_type, const char* column, int32_t* out_index) {
   if (!q) return fail(PINOT_AMD_EINVAL, "add_aggregation: null query");
-  if (agg_type < PINOT_AMD_AGG_COUNT || agg_type > PINOT_AMD_AGG_AVG)
+  if (agg_type < PINOT_AMD_AGG_COUNT || agg_type > PINOT_AMD_AGG_MINMAXRANGE)
     return fail(PINOT_AMD_EINVAL, "add_aggregation: bad type");
   AggSpec a{agg_type, (column && strcmp(column, "*") != 0) ? column : ""};
   if (agg_type != PINOT_AMD_AGG_COUNT && a.column.empty()) return fail(PINOT_AMD_EINVAL, "add_aggregation: column required");
@@ -691,11 +718,47 @@ int pinot_amd_query_add_aggregation_expr(pinot_amd_query* q, int32_t agg_type, i
   if (expr_op < PINOT_AMD_EXPR_MUL || expr_op > PINOT_AMD_EXPR_ADD)
     return fail(PINOT_AMD_EINVAL, "add_aggregation_expr: bad expression op %d", expr_op);
   if (agg_type != PINOT_AMD_AGG_SUM && agg_type != PINOT_AMD_AGG_MIN && agg_type != PINOT_AMD_AGG_MAX &&
-      agg_type != PINOT_AMD_AGG_AVG)
+      agg_type != PINOT_AMD_AGG_AVG && agg_type != PINOT_AMD_AGG_MINMAXRANGE)
     return fail(PINOT_AMD_EUNSUPPORTED, "add_aggregation_expr: aggregation %d over an expression", agg_type);
   AggSpec a{agg_type, column_a, expr_op, column_b};
   if (out_index) *out_index = (int32_t)q->aggs.size();
   q->aggs.push_back(a);
+  return 0;
+}
+
+int pinot_amd_query_set_group_key_values(pinot_amd_query* q, const char* column, int32_t stored_type, int64_t n,
+                                         const int64_t* h_values_i, const double* h_values_d,
+                                         const char* const* h_values_s) {
+  if (!q || !column || n < 0 || stored_type < T_INT || stored_type > T_STRING)
+    return fail(PINOT_AMD_EINVAL, "set_group_key_values: bad arguments");
+  MergedKeyColumn m;
+  m.type = stored_type;
+  for (int64_t i = 0; i < n; ++i) {
+    if (stored_type == T_STRING) {
+      if (!h_values_s || !h_values_s[i]) return fail(PINOT_AMD_EINVAL, "set_group_key_values: null string");
+      m.vs.push_back(h_values_s[i]);
+    } else if (is_float(stored_type)) {
+      if (!h_values_d) return fail(PINOT_AMD_EINVAL, "set_group_key_values: no values");
+      m.vd.push_back(stored_type == T_FLOAT ? (double)(float)h_values_d[i] : h_values_d[i]);
+    } else {
+      if (!h_values_i) return fail(PINOT_AMD_EINVAL, "set_group_key_values: no values");
+      m.vi.push_back(h_values_i[i]);
+    }
+  }
+  // the caller's values in any order: sorted and deduplicated in dictionary order
+  if (m.type == T_STRING) {
+    std::sort(m.vs.begin(), m.vs.end(), java_less);
+    m.vs.erase(std::unique(m.vs.begin(), m.vs.end()), m.vs.end());
+  } else if (is_float(m.type)) {
+    std::sort(m.vd.begin(), m.vd.end(), java_double_less);
+    m.vd.erase(std::unique(m.vd.begin(), m.vd.end(),
+                           [](double a, double b) { return java_double_order(a) == java_double_order(b); }),
+               m.vd.end());
+  } else {
+    std::sort(m.vi.begin(), m.vi.end());
+    m.vi.erase(std::unique(m.vi.begin(), m.vi.end()), m.vi.end());
+  }
+  q->key_space[column] = std::move(m);
   return 0;
 }
 
@@ -710,14 +773,6 @@ int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit) {
 // ------------------------------------------------------------------------------------------------
 // Result / compiled plan
 // ------------------------------------------------------------------------------------------------
-struct MergedKeyColumn {
-  int32_t type = 0;
-  std::vector<int64_t> vi;
-  std::vector<double> vd;
-  std::vector<std::string> vs;
-  size_t size() const { return type == T_STRING ? vs.size() : is_float(type) ? vd.size() : vi.size(); }
-};
-
 // One kernel launch of a plan: the segments of a batch that share a shape (every slot's encoding and
 // fixed-bit width), with their own descriptors and query-specialised kernels. Segments whose
 // columns are encoded differently (a table whose index config changed between segments) run in
@@ -769,7 +824,8 @@ struct pinot_amd_result {
   DevBuf matched;
   std::vector<MergedKeyColumn> keys;  // merged dictionaries of the group-by columns
   std::vector<int64_t> key_stride;    // dense: mixed-radix strides
-  std::vector<int32_t> agg_acc;        // aggregation -> accumulator index (AVG: sum acc)
+  std::vector<int32_t> agg_acc;        // aggregation -> accumulator index (AVG: sum acc; MINMAXRANGE: min acc)
+  std::vector<int32_t> agg_acc2;       // MINMAXRANGE: max acc
   std::vector<int32_t> agg_type;
   int32_t num_group_by = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1094,22 +1150,6 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
   return 0;
 }
 
-// Double.compare / Double.doubleToLongBits order: -0.0 < 0.0, every NaN equal and greatest. Group
-// keys of FLOAT/DOUBLE columns are told apart this way (fastutil's Double2IntOpenHashMap compares
-// doubleToLongBits; sorted dictionaries use Double.compare), so merged key columns sort by it.
-static uint64_t java_double_order(double v) {
-  uint64_t b;
-  if (std::isnan(v)) b = 0x7ff8000000000000ull;
-  else memcpy(&b, &v, 8);
-  return (b >> 63) ? ~b : (b | (1ull << 63));
-}
-static double java_double_from_order(uint64_t k) {
-  uint64_t b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
-  double v;
-  memcpy(&v, &b, 8);
-  return v;
-}
-static bool java_double_less(double a, double b) { return java_double_order(a) < java_double_order(b); }
 
 // GROUP BY on a raw (no-dictionary) column: NoDictionarySingleColumnGroupKeyGenerator /
 // NoDictionaryMultiColumnGroupKeyGenerator (pinot-core/.../query/aggregation/groupby/
@@ -1456,9 +1496,26 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   r->num_group_by = (int32_t)Q.group_by.size();
   r->limit = Q.num_groups_limit;
   double dense_keys = 1;
-  for (auto& g : Q.group_by) {
+  for (size_t j = 0; j < Q.group_by.size(); ++j) {
+    const std::string& g = Q.group_by[j];
     MergedKeyColumn m;
     if (int rc = build_merged_keys(segs, g, &m)) return rc;
+    auto ks = qq->key_space.find(qq->group_by[j]);  // installed key space (original column name)
+    if (ks != qq->key_space.end()) {
+      // it must hold every value of the batch's dictionaries: the batch's merged keys are a subset
+      const MergedKeyColumn& K = ks->second;
+      if (K.type != m.type) return fail(PINOT_AMD_EINVAL, "key space of %s has the wrong type", g.c_str());
+      bool ok = true;
+      if (m.type == T_STRING) {
+        for (auto& v : m.vs) ok &= std::binary_search(K.vs.begin(), K.vs.end(), v, java_less);
+      } else if (is_float(m.type)) {
+        for (double v : m.vd) ok &= std::binary_search(K.vd.begin(), K.vd.end(), v, java_double_less);
+      } else {
+        for (int64_t v : m.vi) ok &= std::binary_search(K.vi.begin(), K.vi.end(), v);
+      }
+      if (!ok) return fail(PINOT_AMD_EINVAL, "key space of %s misses values of the segments' dictionaries", g.c_str());
+      m = K;
+    }
     r->key_stride.push_back((int64_t)std::min(dense_keys, 9.0e18));
     dense_keys *= (double)std::max<size_t>(m.size(), 1);
     r->keys.push_back(std::move(m));
@@ -1480,9 +1537,19 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   r->limit_possible = limit_possible;
 
   // ---- accumulators: acc 0 = COUNT; others grouped by slot; ACC_FIRST_DOC last ----
-  struct AccReq { int slot; int op; int expr; int slot2; };
+  // nan_skip: MinMaxRangePair.apply compares with < / >, so NaN never enters the pair (MIN / MAX of
+  // an aggregation-only query propagate it like Math.min / Math.max)
+  struct AccReq { int slot; int op; int expr; int slot2; int nan_skip; };
   std::vector<AccReq> reqs;
-  std::vector<int> agg_req(Q.aggs.size(), -1);
+  std::vector<int> agg_req(Q.aggs.size(), -1), agg_req2(Q.aggs.size(), -1);
+  auto find_req = [&](const AccReq& rq) -> int {
+    for (size_t k = 0; k < reqs.size(); ++k)
+      if (reqs[k].slot == rq.slot && reqs[k].op == rq.op && reqs[k].expr == rq.expr && reqs[k].slot2 == rq.slot2 &&
+          reqs[k].nan_skip == rq.nan_skip)
+        return (int)k;
+    reqs.push_back(rq);
+    return (int)reqs.size() - 1;
+  };
   for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
     const AggSpec& a = Q.aggs[ai];
     if (a.type == PINOT_AMD_AGG_COUNT) continue;
@@ -1504,21 +1571,20 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         op = ACC_SUM_I64;
         break;
       case PINOT_AMD_AGG_MIN: op = ACC_MIN; break;
+      case PINOT_AMD_AGG_MINMAXRANGE: op = ACC_MIN; break;  // + ACC_MAX below
       default: op = ACC_MAX; break;
     }
     const int sl = slot_of(a.column);
     const int sl2 = a.expr != PINOT_AMD_EXPR_COLUMN ? slot_of(a.column2) : -1;
-    int found = -1;
-    for (size_t k = 0; k < reqs.size(); ++k)
-      if (reqs[k].slot == sl && reqs[k].op == op && reqs[k].expr == a.expr && reqs[k].slot2 == sl2) found = (int)k;
-    if (found < 0) {
-      reqs.push_back({sl, op, a.expr, sl2});
-      found = (int)reqs.size() - 1;
+    if (a.type == PINOT_AMD_AGG_MINMAXRANGE) {
+      agg_req[ai] = find_req({sl, ACC_MIN, a.expr, sl2, 1});
+      agg_req2[ai] = find_req({sl, ACC_MAX, a.expr, sl2, 1});
+    } else {
+      agg_req[ai] = find_req({sl, op, a.expr, sl2, 0});
     }
-    agg_req[ai] = found;
   }
   std::vector<int> req_acc(reqs.size());
-  std::vector<AccReq> acc_req(kMaxAcc + 2, AccReq{0, 0, 0, -1});
+  std::vector<AccReq> acc_req(kMaxAcc + 2, AccReq{0, 0, 0, -1, 0});
   int nacc = 1;
   q.acc_op[0] = ACC_COUNT;
   auto push_acc = [&](const AccReq& rq) -> int {
@@ -1533,11 +1599,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         req_acc[k] = nacc;
         if (int rc = push_acc(reqs[k])) return rc;
         if (reqs[k].op == ACC_SUM_I128)
-          if (int rc = push_acc({reqs[k].slot, ACC_HI, reqs[k].expr, reqs[k].slot2})) return rc;
+          if (int rc = push_acc({reqs[k].slot, ACC_HI, reqs[k].expr, reqs[k].slot2, 0})) return rc;
       }
   for (size_t ai = 0; ai < Q.aggs.size(); ++ai) {
     r->agg_type.push_back(Q.aggs[ai].type);
     r->agg_acc.push_back(agg_req[ai] < 0 ? 0 : req_acc[agg_req[ai]]);
+    r->agg_acc2.push_back(agg_req2[ai] < 0 ? 0 : req_acc[agg_req2[ai]]);
   }
 
   // ---- plan kind ----
@@ -1557,7 +1624,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   if (r->trim) {
     r->fd_acc = nacc;
-    if (int rc = push_acc({-1, ACC_FIRST_DOC, 0, -1})) return rc;
+    if (int rc = push_acc({-1, ACC_FIRST_DOC, 0, -1, 0})) return rc;
   }
   q.nacc = (Q.aggs.empty() && Q.group_by.empty()) ? 0 : nacc;  // filter-only: count matches
   if (filter_only) q.nacc = 0;
@@ -1709,7 +1776,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     base.group.push_back({slot_of(Q.group_by[j]), r->kind == PLAN_HASH ? 0 : r->key_stride[j]});
     for (int si = 0; si < n; ++si) base.any_remap |= hsegs[si].cols[slot_of(Q.group_by[j])].remap != nullptr;
   }
-  for (int a = 1; a < q.nacc; ++a) base.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2});
+  for (int a = 1; a < q.nacc; ++a)
+    base.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2, acc_req[a].nan_skip});
   base.num_keys = num_keys;
   base.bitset = filter_only;
   base.aggregate = q.nacc > 0;
@@ -2287,6 +2355,9 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
         case PINOT_AMD_AGG_MAX:
           v = decode_ordered(w, op);
           break;
+        case PINOT_AMD_AGG_MINMAXRANGE:  // MinMaxRangeAggregationFunction.extractFinalResult: max - min
+          v = decode_ordered(A[r->agg_acc2[a]], ACC_MAX) - decode_ordered(w, ACC_MIN);
+          break;
         default:
           if (op == ACC_SUM_F64) {
             memcpy(&v, &w, 8);
@@ -2299,6 +2370,45 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
       }
       if (h_values) h_values[g * na + a] = v;
       if (h_values_i64) h_values_i64[g * na + a] = vi;
+    }
+  }
+  *h_num_fetched = r->ngroups;
+  return 0;
+}
+
+int pinot_amd_result_fetch_intermediate(pinot_amd_result* r, int64_t cap, double* h_pairs, int64_t* h_num_fetched) {
+  if (!r || cap < 0 || !h_pairs || !h_num_fetched) return fail(PINOT_AMD_EINVAL, "fetch_intermediate: bad arguments");
+  if (int rc = no_throw("fetch_intermediate", [&] { return compact_groups(r); })) return rc;
+  if (r->ngroups > cap)
+    return fail(PINOT_AMD_EOVERFLOW, "fetch_intermediate: %lld groups exceed capacity %lld", (long long)r->ngroups,
+                (long long)cap);
+  const int na = (int)r->agg_type.size();
+  const int nacc = std::max(r->q.nacc, 1);
+  std::vector<double> v((size_t)r->ngroups * na);
+  std::vector<int64_t> vi((size_t)r->ngroups * na);
+  int64_t got = 0;
+  if (int rc = pinot_amd_result_fetch(r, r->ngroups, nullptr, v.data(), vi.data(), &got)) return rc;
+  for (int64_t g = 0; g < r->ngroups; ++g) {
+    const uint64_t* A = &r->cacc[(size_t)g * nacc];
+    for (int a = 0; a < na; ++a) {
+      double* out = h_pairs + ((size_t)g * na + a) * 2;
+      const int acc = r->agg_acc[a];
+      switch (r->agg_type[a]) {
+        case PINOT_AMD_AGG_AVG: {  // AvgPair(sum, count)
+          const double cnt = (double)(r->q.nacc ? A[0] : 0);
+          if (r->q.acc_op[acc] == ACC_SUM_F64) memcpy(&out[0], &A[acc], 8);
+          else out[0] = (double)(__int128)(((unsigned __int128)A[acc + 1] << 64) | (unsigned __int128)A[acc]);
+          out[1] = cnt;
+          break;
+        }
+        case PINOT_AMD_AGG_MINMAXRANGE:  // MinMaxRangePair(min, max)
+          out[0] = decode_ordered(A[acc], ACC_MIN);
+          out[1] = decode_ordered(A[r->agg_acc2[a]], ACC_MAX);
+          break;
+        default:
+          out[0] = v[(size_t)g * na + a];
+          out[1] = 0;
+      }
     }
   }
   *h_num_fetched = r->ngroups;

@@ -40,6 +40,7 @@ struct JitAcc {
   int slot;
   int expr = EXPR_COL;
   int slot2 = -1;
+  int nan_skip = 0;  // aggregation-only MIN / MAX: NaN skipped (MinMaxRangePair) instead of propagated
   JitVal val() const { return JitVal{expr, slot, slot2}; }
 };
 struct JitPlan {

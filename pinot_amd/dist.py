@@ -5,15 +5,16 @@ in the broker (BrokerReduceService). Here every GPU executes its shard of segmen
 accumulator table over the query's merged key space (accumulation across its own segments happens
 in-kernel), and the tables of all GPUs are merged in place with RCCL all-reduces over xGMI:
 SUM/COUNT as int64 or fp64 sums, MIN/MAX as min/max of an order-preserving int64 encoding of the
-double value. One all-reduce per accumulator array; no other data-path collective.
+double value. Small tables go through one all-gather reduced locally; no other data-path collective.
 
-The merge is valid when every rank's merged dictionaries of the group-by columns agree (the
-segments share a table's dictionaries or the union is installed on all ranks);
-``key_space_fingerprint`` lets callers assert that before merging.
+Every rank plans the query over the same group key space: ``global_key_space`` all-gathers each
+rank's group-by column values and the union is installed on every rank
+(``pinot_amd_query_set_group_key_values``), so dense tables index identical groups whatever each
+rank's own dictionaries hold. Results without a dense table (hash-table GROUP BY, DISTINCTCOUNT)
+merge by value like the broker (``merge_groups``).
 """
 from __future__ import annotations
 
-import ctypes as C
 import hashlib
 import os
 from typing import List, Sequence
@@ -69,18 +70,49 @@ def _from_limbs(l):
     return lo, hi
 
 
-def merge_tables(table, ops: Sequence[int], num_keys: int, group=None) -> None:
-    """In-place all-reduce of a [len(ops), num_keys] int64 tensor of accumulator words.
+def _reduce_gathered(g, ops):
+    """[world, len(ops), num_keys] gathered tables -> the merged [len(ops), num_keys] table (the same
+    reductions merge_tables' all-reduces perform)."""
+    import torch
+    out = g[0].clone()
+    for i, op in enumerate(ops):
+        if op == OP_SUM_I64:
+            out[i] = g[:, i].sum(0)
+        elif op == OP_SUM_F64:
+            out[i] = g[:, i].contiguous().view(torch.float64).sum(0).view(torch.int64)
+        elif op == OP_SUM_I128:
+            lo, hi = _from_limbs(_limbs(g[:, i], g[:, i + 1]).sum(1))
+            out[i] = lo
+            out[i + 1] = hi
+        elif op in (OP_MIN, OP_MAX):
+            s_ = g[:, i] ^ SIGN
+            out[i] = (s_.amin(0) if op == OP_MIN else s_.amax(0)) ^ SIGN
+    return out
+
+
+def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_max_bytes: int = 1 << 20) -> None:
+    """In-place merge across ranks of a [len(ops), num_keys] int64 tensor of accumulator words.
 
     ops per row: 0 = int64 sum, 1 = fp64 sum (words are double bits), 2/3 = min/max of the
     library's ordered-uint64 encoding (flipping the sign bit makes it an order-preserving int64),
-    4/5 = low/high word of an exact 128-bit integer sum (all-reduced as 32-bit limbs).
-    One collective per reduction kind: all integer sums (int64 rows and the limbs of 128-bit rows) in
-    one int64 SUM, double sums in one fp64 SUM, and one MIN / one MAX."""
+    4/5 = low/high word of an exact 128-bit integer sum (reduced as 32-bit limbs).
+
+    Tables up to gather_max_bytes: ONE all-gather of the whole table, reduced locally per row kind
+    (a latency-bound exchange: one collective instead of one per reduction kind). Larger tables: one
+    all-reduce per reduction kind (integer sums incl. the limbs of 128-bit rows in one int64 SUM, double
+    sums in one fp64 SUM, one MIN, one MAX), each moving ~2x the table per rank on a ring."""
     import torch
     import torch.distributed as dist
     t = table.view(len(ops), num_keys)
     ops = list(ops)
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    if t.numel() * 8 <= gather_max_bytes:
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t.contiguous(), group=group)
+        t.copy_(_reduce_gathered(torch.stack(parts), ops))
+        return
     i64 = [i for i, op in enumerate(ops) if op == OP_SUM_I64]
     i128 = [i for i, op in enumerate(ops) if op == OP_SUM_I128]
     f64 = [i for i, op in enumerate(ops) if op == OP_SUM_F64]
@@ -107,36 +139,89 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None) -> None:
             t[rows] = s_ ^ SIGN
 
 
-_hip = None
+class _DeviceWords:
+    """A library-owned HBM array seen by torch without a copy (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2,
+                                         "strides": None}
 
 
-def _hip_memcpy(dst: int, src: int, nbytes: int, stream=None) -> None:
-    """Device-to-device copy through the process's (torch-loaded) HIP runtime."""
-    global _hip
-    if _hip is None:
-        _hip = C.CDLL("libamdhip64.so.7")
-        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
-        _hip.hipMemcpyAsync.restype = C.c_int
-    rc = _hip.hipMemcpyAsync(dst, src, nbytes, 3, stream)  # hipMemcpyDeviceToDevice
-    if rc != 0:
-        raise RuntimeError(f"hipMemcpyAsync failed: {rc}")
-
-
-def merge_result(result, scratch=None, group=None, stream=None):
-    """All-reduce a QueryResult's dense accumulators across ranks (in place). Returns the scratch
-    tensor so callers can reuse it across steps."""
+def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes: int = 1 << 20):
+    """Merge a QueryResult's dense accumulators across ranks, in place in the library's HBM table (a
+    zero-copy torch view of it; rows are contiguous in one allocation). The result must have been
+    executed on torch's current stream (or that stream synchronised). Every rank must have run the
+    query over the same key space (global_key_space). `scratch` is unused (kept for callers)."""
     import torch
     ops, nk, ptrs = result.accumulators()
     if not ops:
         return scratch
-    n = len(ops) * nk
-    if scratch is None or scratch.numel() != n:
-        scratch = torch.empty(n, dtype=torch.int64, device="cuda")
-    sh = None if stream is None else int(getattr(stream, "cuda_stream", stream))
-    _hip_memcpy(scratch.data_ptr(), ptrs[0], n * 8, sh)  # rows are contiguous in one allocation
-    merge_tables(scratch, ops, nk, group)
-    _hip_memcpy(ptrs[0], scratch.data_ptr(), n * 8, sh)
+    table = torch.as_tensor(_DeviceWords(ptrs[0], len(ops) * nk), device="cuda")
+    assert table.data_ptr() == ptrs[0], "zero-copy view of the accumulator table failed"
+    merge_tables(table, ops, nk, group, gather_max_bytes)
     return scratch
+
+
+def merge_groups(qc, groups: dict, group=None) -> dict:
+    """Broker-style merge by value (GroupByDataTableReducer.java:258 / AggregationFunction.merge) of
+    every rank's fetched groups: for results without a shared dense table (hash-table GROUP BY,
+    DISTINCTCOUNT sets). Returns the merged groups on every rank."""
+    import torch.distributed as dist
+    from .query import merge_partial
+    world = dist.get_world_size(group)
+    parts = [None] * world
+    dist.all_gather_object(parts, groups, group=group)
+    out: dict = {}
+    for g in parts:
+        for k, v in g.items():
+            out[k] = [merge_partial(a.func, x, y) for a, x, y in zip(qc.aggregations, out[k], v)] if k in out else v
+    return out
+
+
+def local_key_values(segments, column: str, executor=None) -> list:
+    """Distinct values of a group-by column over this rank's segments: the dictionaries of
+    dictionary-encoded columns; raw columns' values through a device GROUP BY over all docs."""
+    from .query import distinct_value
+    vals = {}
+    raw = []
+    for s in segments:
+        cb = s.columns[column]
+        if cb.has_dictionary:
+            for v in cb.dict_values.tolist():
+                vals.setdefault(distinct_value(v), v)
+        else:
+            raw.append(s)
+    if raw:
+        from .engine import ServerQueryExecutor
+        ex = executor or ServerQueryExecutor()
+        res = ex.execute(f"SET numGroupsLimit = {1 << 40}; SELECT {column}, COUNT(*) FROM t GROUP BY {column}", raw)
+        for (v,) in res.groups():
+            vals.setdefault(distinct_value(v), v)
+        res.destroy()
+    return list(vals.values())
+
+
+def global_key_space(segments, group_by: Sequence[str], group=None, executor=None) -> dict:
+    """Union over all ranks of every group-by column's values (one all-gather of the value lists),
+    to install with ServerQueryExecutor.execute(..., key_space=...) so that every rank's dense group
+    table indexes the same groups and merge_result can all-reduce them in place."""
+    import torch.distributed as dist
+    from .query import distinct_value
+    mine = {g: local_key_values(segments, g, executor) for g in group_by}
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    parts = [None] * world
+    if world > 1:
+        dist.all_gather_object(parts, mine, group=group)
+    else:
+        parts = [mine]
+    out = {}
+    for g in group_by:
+        u = {}
+        for p in parts:
+            for v in p[g]:
+                u.setdefault(distinct_value(v), v)
+        out[g] = list(u.values())
+    return out
 
 
 def key_space_fingerprint(segments, group_by: Sequence[str]) -> str:

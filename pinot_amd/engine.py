@@ -24,13 +24,13 @@ import numpy as np
 
 from . import _lib
 from ._lib import ColumnSpec, PredicateSpec, check, lib
-from .query import QueryContext, fold_distinct_count, parse_sql, reduce_rows, split_distinct_count
+from .query import JavaDouble, QueryContext, fold_distinct_count, parse_sql, reduce_rows, split_distinct_count
 from .segment import ColumnBuffers, SegmentBuffers, DOUBLE, FLOAT, INT, LONG, STRING
 
 TYPE_CODE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3, STRING: 4}
 ENC_CODE = {"FIXED_BIT": 0, "RAW": 1, "SORTED": 2}
 PRED_CODE = {"EQ": 0, "NOT_EQ": 1, "IN": 2, "NOT_IN": 3, "RANGE": 4}
-AGG_CODE = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4, "AVG": 5}
+AGG_CODE = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "SUMLONG": 4, "AVG": 5, "MINMAXRANGE": 6}
 EXPR_CODE = {"MUL": 1, "SUB": 2, "ADD": 3}
 
 
@@ -171,11 +171,32 @@ class DistinctCountResult:
     def kernel_info(self) -> str:
         return self._base.kernel_info()
 
+    def _all(self):
+        return [self._base] + [r for _, r in self._subs]
+
     def groups(self):
         return fold_distinct_count(self.qc, self._base.groups(), [(i, r.groups()) for i, r in self._subs])
 
     def rows(self):
         return reduce_rows(self.qc, self.groups())
+
+    def execute_again(self, stream=None) -> None:
+        for r in self._all():
+            r.execute_again(stream)
+
+    def last_kernel_ms(self) -> float:
+        return sum(r.last_kernel_ms() for r in self._all())
+
+    def algorithmic_bytes(self) -> float:
+        return sum(r.algorithmic_bytes() for r in self._all())
+
+    def accumulators(self):
+        raise NotImplementedError("DISTINCTCOUNT results merge as value sets (groups()), not as accumulator "
+                                  "tables: the cross-GPU merge of dist.merge_result is single-rank only for them")
+
+    def destroy(self) -> None:
+        for r in self._all():
+            r.destroy()
 
 
 class QueryResult:
@@ -242,6 +263,12 @@ class QueryResult:
         check(L.pinot_amd_result_fetch(self._h, n, keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                        vals.ctypes.data_as(C.POINTER(C.c_double)),
                                        vals_i.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(got)), "fetch")
+        pairs = None
+        if any(s[0] == "range" for s in self._agg_slots):
+            pairs = np.zeros(n * nnat * 2, dtype=np.float64)
+            got2 = C.c_int64()
+            check(L.pinot_amd_result_fetch_intermediate(self._h, n, pairs.ctypes.data_as(C.POINTER(C.c_double)),
+                                                        C.byref(got2)), "fetch_intermediate")
         out = {}
         for g in range(got.value):
             key = []
@@ -251,7 +278,7 @@ class QueryResult:
                 if t == STRING:
                     key.append(L.pinot_amd_result_string_key(self._h, j, raw).decode())
                 elif t in (FLOAT, DOUBLE):
-                    key.append(float(np.int64(raw).view(np.float64)))
+                    key.append(JavaDouble(np.int64(raw).view(np.float64)))
                 else:
                     key.append(raw)
             parts = []
@@ -261,7 +288,8 @@ class QueryResult:
                     c = vals_i[g * nnat + slot[2]]
                     parts.append((float(s), int(c)))
                 elif slot[0] == "range":
-                    parts.append((float(vals[g * nnat + slot[1]]), float(vals[g * nnat + slot[2]])))
+                    o = (g * nnat + slot[1]) * 2
+                    parts.append((float(pairs[o]), float(pairs[o + 1])))
                 elif a.func in ("COUNT", "SUMLONG"):
                     parts.append(int(vals_i[g * nnat + slot[1]]))
                 else:
@@ -338,15 +366,31 @@ class ServerQueryExecutor:
             raise
         return qh
 
-    def execute(self, query, segments: Sequence[ImmutableSegment], stream=None):
+    def execute(self, query, segments: Sequence[ImmutableSegment], stream=None, key_space=None):
+        """Run a query over HBM-resident segments. key_space (optional): group-by column -> the values of
+        its global key space (dist.global_key_space: the union of every rank's dictionaries), so that
+        every rank's dense group table indexes the same groups."""
         qc = parse_sql(query) if isinstance(query, str) else query
         if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):
             base, subs = split_distinct_count(qc)
-            return DistinctCountResult(qc, self._execute(base, segments, stream),
-                                       [(i, self._execute(sq, segments, stream)) for i, sq in subs])
-        return self._execute(qc, segments, stream)
+            return DistinctCountResult(qc, self._execute(base, segments, stream, key_space),
+                                       [(i, self._execute(sq, segments, stream, key_space)) for i, sq in subs])
+        return self._execute(qc, segments, stream, key_space)
 
-    def _execute(self, qc, segments: Sequence[ImmutableSegment], stream=None) -> QueryResult:
+    @staticmethod
+    def _set_key_space(qh, column: str, stored_type: str, values) -> None:
+        n = len(values)
+        vi = vd = vs = None
+        if stored_type == STRING:
+            vs = (C.c_char_p * max(n, 1))(*[str(v).encode() for v in values])
+        elif stored_type in (FLOAT, DOUBLE):
+            vd = (C.c_double * max(n, 1))(*[float(v) for v in values])
+        else:
+            vi = (C.c_int64 * max(n, 1))(*[int(v) for v in values])
+        check(lib().pinot_amd_query_set_group_key_values(qh, column.encode(), TYPE_CODE[stored_type], n, vi, vd, vs),
+              f"set_group_key_values({column})")
+
+    def _execute(self, qc, segments: Sequence[ImmutableSegment], stream=None, key_space=None) -> QueryResult:
         if not segments:
             raise ValueError("no segments")
         L = lib()
@@ -364,6 +408,8 @@ class ServerQueryExecutor:
                     check(L.pinot_amd_query_add_predicate(qh, ci, C.byref(spec), 1 if neg else 0), "add_predicate")
             for g in qc.group_by:
                 check(L.pinot_amd_query_add_group_by(qh, g.encode()), "add_group_by")
+                if key_space is not None and g in key_space:
+                    self._set_key_space(qh, g, first.columns[g].stored_type, key_space[g])
             check(L.pinot_amd_query_set_num_groups_limit(qh, qc.num_groups_limit), "set_num_groups_limit")
             native = []
             agg_slots = []
@@ -386,8 +432,8 @@ class ServerQueryExecutor:
             for a in qc.aggregations:
                 if a.func == "AVG":
                     agg_slots.append(("avg", add("SUM", a.column, a.expr), add("COUNT", "*")))
-                elif a.func == "MINMAXRANGE":  # MinMaxRangePair = (MIN, MAX) accumulators
-                    agg_slots.append(("range", add("MIN", a.column, a.expr), add("MAX", a.column, a.expr)))
+                elif a.func == "MINMAXRANGE":  # MinMaxRangePair (min, max), NaN-skipping, in the library
+                    agg_slots.append(("range", add("MINMAXRANGE", a.column, a.expr)))
                 else:
                     agg_slots.append(("direct", add(a.func, a.column, a.expr)))
             if not qc.aggregations and qc.group_by:

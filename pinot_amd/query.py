@@ -10,8 +10,12 @@ literals, comparisons, BETWEEN, [NOT] IN, AND/OR/NOT); anything else raises Valu
 from __future__ import annotations
 
 import dataclasses
+import math
 import re
+import struct
 from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
 
 AGG_FUNCS = ("COUNT", "SUM", "MIN", "MAX", "AVG", "SUMLONG", "MINMAXRANGE", "DISTINCTCOUNT")
 DEFAULT_GROUP_BY_LIMIT = 10          # Pinot's default LIMIT for group-by results
@@ -458,21 +462,63 @@ def split_distinct_count(qc: QueryContext):
     return base, subs
 
 
+_NAN_BITS = 0x7FF8000000000000
+
+
+def distinct_value(v):
+    """The identity of a value in DISTINCTCOUNT's set and in a group key: FLOAT/DOUBLE values compare
+    by Double.doubleToLongBits (every NaN one value, -0.0 != 0.0: the fastutil Double/Float open hash
+    sets of DistinctCountAggregationFunction), so floats become their canonical 64-bit pattern; other
+    values are themselves."""
+    if isinstance(v, (float, np.floating)):
+        f = float(v)
+        return ("f", _NAN_BITS if math.isnan(f) else struct.unpack("<q", struct.pack("<d", f))[0])
+    return v
+
+
+class JavaDouble(float):
+    """A FLOAT/DOUBLE group-key value with Java's key identity (Double.equals / doubleToLongBits, as the
+    group-key maps use): every NaN equals every NaN and -0.0 != 0.0, so dicts keyed by group tuples
+    keep the groups Pinot keeps apart. Arithmetic and ordering are a float's."""
+    __slots__ = ()
+
+    def __eq__(self, other):
+        if isinstance(other, float):
+            return distinct_value(float(self)) == distinct_value(float(other))
+        return float.__eq__(self, other)
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    def __hash__(self):  # consistent with float's hash where the identities agree
+        return hash(_NAN_BITS) if math.isnan(self) else float.__hash__(self)
+
+    def __repr__(self):
+        return float.__repr__(self)
+
+
+def canonical_key(key) -> tuple:
+    return tuple(distinct_value(v) for v in key)
+
+
 def fold_distinct_count(qc: QueryContext, base_groups: dict, sub_groups: Sequence[Tuple[int, dict]]) -> dict:
     """Groups of the original query from split_distinct_count's results (same group keys as the
-    base query: a group exists iff a doc matched, in every one of the queries alike)."""
+    base query: a group exists iff a doc matched, in every one of the queries alike). Keys and set
+    elements are matched by distinct_value (bit patterns for floats), never by Python float equality."""
     sets = {i: {} for i, _ in sub_groups}
     for i, g in sub_groups:
         for key in g:
-            sets[i].setdefault(tuple(key[:-1]), set()).add(key[-1])
+            sets[i].setdefault(canonical_key(key[:-1]), set()).add(distinct_value(key[-1]))
     rest_idx = [j for j, a in enumerate(qc.aggregations) if a.func != "DISTINCTCOUNT"]
     out = {}
     for key, parts in base_groups.items():
         full = [None] * len(qc.aggregations)
         for j, p in zip(rest_idx, parts):
             full[j] = p
+        ck = canonical_key(key)
         for i in sets:
-            full[i] = frozenset(sets[i].get(tuple(key), ()))
+            full[i] = frozenset(sets[i].get(ck, ()))
         out[key] = full
     return out
 

@@ -179,3 +179,113 @@ def test_int128_limbs_round_trip():
     l = _limbs(torch.from_numpy(lo), torch.from_numpy(hi))
     a, b = _from_limbs(l)
     assert _from_words(a.numpy(), b.numpy()) == vals
+
+
+# ------------------------------------------------ disjoint dictionaries: global key space + both merges
+def _disjoint_segments():
+    """Six segments whose d1 dictionaries differ segment to segment: shard r of 2 holds values the
+    other shard never sees (and some it does)."""
+    from pinot_amd.segment import DOUBLE, INT, LONG, build_segment
+    rng = np.random.default_rng(7)
+    out = []
+    for i in range(6):
+        n = int(rng.integers(2000, 9000))
+        d1 = rng.integers(0, 30, n) * 10 + (i % 2) * 1000 + (i // 2)   # ranks 0/1 disjoint ranges
+        d1[:5] = [5, 15, 25, 35, 45]                                    # + a shared set
+        out.append(build_segment(f"dj{i}", {
+            "d0": (rng.integers(0, 5000, n).astype(np.int32), INT, {}),
+            "d1": (d1.astype(np.int32), INT, {}),
+            "r_long": (rng.integers(-(1 << 40), 1 << 40, n), LONG, {"dictionary": False}),
+            "r_double": (rng.normal(0, 1000, n), DOUBLE, {"dictionary": False}),
+            "r_int": (rng.integers(-10 ** 6, 10 ** 6, n).astype(np.int32), INT, {"dictionary": False})}))
+    return out
+
+
+def _disjoint_worker(rank, world, port, gather_max_bytes, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle
+    from pinot_amd import dist as pdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = pdist.shard(_disjoint_segments(), rank, world)
+    own = sorted(set().union(*[set(s.columns["d1"].dict_values.tolist()) for s in mine]))
+    ks = pdist.global_key_space(mine, ["d1"])
+    keys = sorted(ks["d1"])
+    assert set(own) < set(keys)  # this rank's own dictionaries do not cover the key space
+    _, groups = oracle.execute(QUERY, mine)
+    table = torch.from_numpy(_dense_table(groups, keys).view(np.int64).ravel().copy())
+    pdist.merge_tables(table, OPS, len(keys), gather_max_bytes=gather_max_bytes)
+    if rank == 0:
+        out.put((keys, table.numpy().view(np.uint64).reshape(5, -1).copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("gather_max_bytes", [0, 1 << 20], ids=["allreduce", "allgather"])
+def test_disjoint_dictionaries_global_key_space(gather_max_bytes):
+    """Ranks with different dictionaries agree on the union key space (global_key_space: one
+    all-gather), so their dense tables merge in place; equal to the single-process oracle group for
+    group, through the per-kind all-reduces and through the single all-gather + local reduction."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_disjoint_worker, args=(r, 2, port, gather_max_bytes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    keys, merged = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    _, exp = oracle.execute(QUERY, _disjoint_segments())
+    assert set(k for (k,) in exp) <= set(keys)
+    for i, k in enumerate(keys):
+        if (k,) not in exp:
+            assert merged[0, i] == 0
+            continue
+        cnt, s_long, s_dbl, mn, mx = exp[(k,)]
+        assert int(merged[0, i]) == cnt
+        assert int(merged[1, i].view(np.int64)) == int(s_long)
+        assert np.isclose(merged[2:3, i].view(np.float64)[0], s_dbl, rtol=1e-12)
+        assert _decode_ordered(merged[3:4, i])[0] == mn
+        assert _decode_ordered(merged[4:5, i])[0] == mx
+
+
+def _gather_i128_worker(rank, world, port, out):
+    from pinot_amd import dist as pdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    vals = _rank_sums(rank)
+    lo, hi = _to_words(vals)
+    cnt = np.full(len(vals), 1000 + rank, dtype=np.int64)
+    table = torch.from_numpy(np.concatenate([cnt, lo, hi]).copy())
+    pdist.merge_tables(table, [pdist.OP_SUM_I64, pdist.OP_SUM_I128, pdist.OP_HI], len(vals), gather_max_bytes=1 << 30)
+    if rank == 0:
+        out.put(table.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_int128_sums_merge_exactly_through_allgather():
+    """The small-table path (one all-gather, local limb reduction) is exact past INT64_MAX too."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_i128_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    merged = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = I128_KEYS + 2
+    exp = [sum(_rank_sums(r)[k] for r in range(4)) for k in range(n)]
+    assert _from_words(merged[n:2 * n], merged[2 * n:3 * n]) == exp
+    assert list(merged[:n]) == [sum(1000 + r for r in range(4))] * n

@@ -1,6 +1,8 @@
 """Sharded execution + cross-process merge on the device path (2 ranks sharing the box's GPU,
-gloo carrying the all-reduces of the library's dense accumulator tables). The RCCL path of bench.py
-uses the same pinot_amd.dist.merge_result with backend 'nccl' on 8 GPUs."""
+gloo carrying the collectives over the library's dense accumulator tables, viewed in place). Each
+rank's segments have their own dictionaries: the ranks agree on the union key space first
+(dist.global_key_space). The RCCL path of bench.py uses the same pinot_amd.dist functions with backend
+'nccl' on 8 GPUs."""
 import os
 import socket
 import sys
@@ -24,8 +26,7 @@ def _segments():
     for i in range(5):
         n = int(rng.integers(5000, 40000))
         d0 = rng.integers(0, 5000, n)
-        d1 = rng.integers(0, 64, n)
-        d1[:64] = np.arange(64)  # every rank sees the same d1 dictionary -> same key space
+        d1 = rng.integers(0, 64, n) + 100 * (i % 2)  # shards 0 / 1 see disjoint d1 dictionaries
         segs.append(build_segment(f"s{i}", {
             "d0": (d0.astype(np.int32), INT, {}),
             "d1": ((d1 * 3 + 1).astype(np.int32), INT, {}),
@@ -36,29 +37,40 @@ def _segments():
     return segs
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, plan):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, ROOT)
     from pinot_amd import dist as pdist, engine
     torch.cuda.set_device(0)
+    if plan == "hash":
+        os.environ["PINOT_AMD_GROUP_PLAN"] = "hash"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     bufs = pdist.shard(_segments(), rank, world)
     fps = [None] * world
     dist.all_gather_object(fps, pdist.key_space_fingerprint(bufs, ["d1"]))
-    assert len(set(fps)) == 1, "ranks disagree on the group key space"
+    assert len(set(fps)) == world, "shards were meant to hold different dictionaries"
     segs = [engine.ImmutableSegment(b) for b in bufs]
-    res = engine.ServerQueryExecutor().execute(QUERY, segs)
-    pdist.merge_result(res)
-    torch.cuda.synchronize()
+    ks = pdist.global_key_space(segs, ["d1"])
+    res = engine.ServerQueryExecutor().execute(QUERY, segs, stream=torch.cuda.current_stream(), key_space=ks)
+    if plan == "dense":
+        assert res.kernel_info().startswith("jit") and "hash" not in res.kernel_info()
+        pdist.merge_result(res, stream=torch.cuda.current_stream(), gather_max_bytes=int(os.environ["GATHER_MAX"]))
+        torch.cuda.synchronize()
+        groups = res.groups()
+    else:  # hash-table GROUP BY: merged by value like the broker
+        assert "hash" in res.kernel_info()
+        from pinot_amd.query import parse_sql
+        groups = pdist.merge_groups(parse_sql(QUERY), res.groups())
     if rank == 0:
-        q.put(res.groups())
+        q.put(groups)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_merge_equals_single_process():
+@pytest.mark.parametrize("plan,gather_max", [("dense", 0), ("dense", 1 << 20), ("hash", 0)])
+def test_two_rank_merge_equals_single_process(plan, gather_max, monkeypatch):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     with socket.socket() as s:
@@ -66,7 +78,8 @@ def test_two_rank_merge_equals_single_process():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    monkeypatch.setenv("GATHER_MAX", str(gather_max))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, plan)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
