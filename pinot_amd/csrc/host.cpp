@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <climits>
 #include <limits>
 #include <map>
 #include <memory>
@@ -27,6 +28,7 @@
 
 namespace pamd {
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st);
+hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long long* out, hipStream_t st);
 hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc, int fd_acc,
                        int32_t nsegs, int64_t limit, const int64_t* bucket_base, uint32_t* hist,
                        unsigned long long* seg_distinct, int64_t* bstar, int64_t* rank, unsigned long long* bitmap,
@@ -177,6 +179,10 @@ struct Column {
   std::vector<double> dict_d;
   std::vector<std::string> dict_s;
   std::vector<int32_t> sorted_start, sorted_end;  // sorted columns
+  // INT / LONG value range (ColumnMetadata minValue / maxValue): dictionary ends, or computed over the
+  // staged raw values; bounds which integer sums fit 64-bit partial accumulators
+  bool has_range = false;
+  int64_t vmin = 0, vmax = 0;
   // inverted index
   DevBuf inv;
   DevBuf inv_conts;
@@ -502,6 +508,22 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
     if (!spec->h_dictionary) return fail(PINOT_AMD_EINVAL, "column %s: dictionary required", spec->name);
     rc = decode_dictionary(*c, (const uint8_t*)spec->h_dictionary, spec->dictionary_size);
     if (rc) return rc;
+    if (!c->dict_i.empty()) {  // INT / LONG dictionaries are sorted
+      c->has_range = true;
+      c->vmin = *std::min_element(c->dict_i.begin(), c->dict_i.end());
+      c->vmax = *std::max_element(c->dict_i.begin(), c->dict_i.end());
+    }
+  } else if ((c->type == T_INT || c->type == T_LONG) && nd > 0) {
+    DevBuf mm;
+    if (int rc2 = mm.alloc(16)) return rc2;
+    const long long init[2] = {LLONG_MAX, LLONG_MIN};
+    HIP_OK(hipMemcpy(mm.p, init, 16, hipMemcpyHostToDevice));
+    HIP_OK(launch_raw_int_minmax((const uint8_t*)c->fwd.p, c->type, nd, (long long*)mm.p, nullptr));
+    long long got[2];
+    HIP_OK(hipMemcpy(got, mm.p, 16, hipMemcpyDeviceToHost));
+    c->has_range = true;
+    c->vmin = got[0];
+    c->vmax = got[1];
   }
   if (spec->h_inverted && spec->inverted_size) {
     if (c->enc == ENC_RAW) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: inverted index on raw column", spec->name);
@@ -1916,6 +1938,33 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
       jp.leaves.push_back(jl);
     }
+    if ((jp.lds || jp.partitioned) && !env_is("PINOT_AMD_NARROW_SUMS", "0")) {
+      // integer SUMs into an LDS table: 64-bit partials when |value| x (docs one block adds) < 2^63.
+      // Scan blocks own ceil(tiles / grid) tiles and grid >= min(CUs, tiles / kPartSub); a partition
+      // aggregation block takes ceil(records / agg_grid) <= ceil(docs / CUs) records.
+      const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, tiles / kPartSub));
+      const __int128 docs_bound = jp.partitioned ? (__int128)((L.docs + cus - 1) / cus)
+                                                 : (__int128)((tiles + min_grid - 1) / min_grid) * kTileDocs;
+      auto maxabs = [&](int sl) -> __int128 {  // over the launch's segments; -1: unknown
+        __int128 m = 0;
+        for (int si : L.segs) {
+          const Column& c = *segs[si]->cols.at(slot_cols[sl]);
+          if (!c.has_range) return -1;
+          m = std::max(m, std::max((__int128)c.vmax < 0 ? -(__int128)c.vmax : (__int128)c.vmax,
+                                   (__int128)c.vmin < 0 ? -(__int128)c.vmin : (__int128)c.vmin));
+        }
+        return m;
+      };
+      for (JitAcc& a : jp.accs) {
+        if (a.op != ACC_SUM_I128) continue;
+        __int128 m = maxabs(a.slot);
+        if (m >= 0 && a.expr != EXPR_COL) {
+          const __int128 m2 = maxabs(a.slot2);
+          m = m2 < 0 ? -1 : a.expr == EXPR_MUL ? m * m2 : m + m2;
+        }
+        a.narrow = (m >= 0 && m * docs_bound <= (__int128)INT64_MAX) ? 1 : 0;
+      }
+    }
     {  // pipeline depth: ~4 KiB in flight per wave (256 docs x bytes per row)
       double bpr = 0;
       for (const JitSlot& js : jp.slots)
@@ -1965,6 +2014,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       ja.vals.clear();
       ja.val_off.clear();
       ja.rec_bytes = ja.stage_cap = ja.nparts = ja.key_shift = 0;
+      for (auto& a : ja.accs) a.narrow = 0;  // HBM table: full 128-bit adds
       if (!env_is("PINOT_AMD_ATOMIC_HANDOVER", "0")) {
         std::string err;
         L.jit_atomic = jit_get(ja, &err);

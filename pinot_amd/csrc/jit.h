@@ -41,6 +41,11 @@ struct JitAcc {
   int expr = EXPR_COL;
   int slot2 = -1;
   int nan_skip = 0;  // aggregation-only MIN / MAX: NaN skipped (MinMaxRangePair) instead of propagated
+  // ACC_SUM_I128 into an LDS table whose per-block partial sums provably fit int64 (the column's value
+  // range x the docs one block (or one aggregation block) can add to a key): the LDS word is a plain
+  // int64 (ds_add_u64, no returned value to wait for) and the flush sign-extends it into the
+  // 128-bit HBM sum
+  int narrow = 0;
   JitVal val() const { return JitVal{expr, slot, slot2}; }
 };
 struct JitPlan {

@@ -776,6 +776,43 @@ hipError_t launch_chunk_decompress(const uint8_t* src, uint8_t* dst, const void*
   return hipGetLastError();
 }
 
+// ColumnMetadata minValue / maxValue of a raw INT / LONG column (SegmentColumnarIndexCreator writes them
+// into metadata.properties): min and max of the staged big-endian values, grid-stride with a wave
+// reduction and one 64-bit atomic pair per wave. out[0] / out[1] start at INT64_MAX / INT64_MIN.
+__global__ void raw_int_minmax_kernel(const uint8_t* __restrict__ be, int type, int64_t n, long long* out) {
+  long long mn = LLONG_MAX, mx = LLONG_MIN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    long long v;
+    if (type == T_INT) {
+      v = (long long)(int32_t)__builtin_bswap32(*reinterpret_cast<const uint32_t*>(be + 4 * i));
+    } else {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(be + 8 * i);
+      v = (long long)(((uint64_t)__builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]));
+    }
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(out, mn);
+    atomicMax(out + 1, mx);
+  }
+}
+
+hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long long* out, hipStream_t st) {
+  unsigned g = grid_for(n, kBlock);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(raw_int_minmax_kernel, dim3(g), dim3(kBlock), 0, st, be, type, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st) {
   const int64_t n = (int64_t)q.nacc * num_keys;
   unsigned g = grid_for(n, kBlock);

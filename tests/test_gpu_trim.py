@@ -193,3 +193,40 @@ def test_mixed_encodings_across_segments(engine):
         assert res.num_docs_matched() == nm
         fs = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "f"}
         assert_same_groups(res.groups(), og, fs)
+
+
+@pytest.mark.parametrize("narrow", ["1", "0"])
+def test_int_sums_narrow_lds_partials(engine, monkeypatch, narrow):
+    """Integer SUMs into LDS tables keep 64-bit partials when the column's value range (dictionary
+    ends, or the min / max computed at staging) times the docs one block can add stays below 2^63,
+    and 128-bit partials otherwise. Both ways give the exact sums: INT values at the type's extremes,
+    LONG values near 2^44 (narrow) and near 2^60 (wide), in the LDS table plan and in the partitioned
+    plan (whose aggregation blocks use the same rule), against the oracle."""
+    monkeypatch.setenv("PINOT_AMD_NARROW_SUMS", narrow)
+    rng = np.random.default_rng(31)
+    bufs = []
+    for i in range(3):
+        n = 120_000 + 17 * i
+        iv = rng.choice(np.array([-(1 << 31), (1 << 31) - 1, 0, 5], dtype=np.int64), n).astype(np.int32)
+        cols = {
+            "g": (rng.integers(0, 50, n).astype(np.int32), S.INT, {}),
+            "a": (rng.integers(0, 700, n).astype(np.int32), S.INT, {}),
+            "b": (rng.integers(0, 700, n).astype(np.int32), S.INT, {}),
+            "i": (iv, S.INT, {"dictionary": False}),
+            "l44": (rng.integers((1 << 44) - 1000, 1 << 44, n, dtype=np.int64), S.LONG, {"dictionary": False}),
+            "l60": (rng.integers(-(1 << 60), 1 << 60, n, dtype=np.int64), S.LONG, {"dictionary": False}),
+            "dl": (rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64) // 4096 * 4096, S.LONG, {}),
+        }
+        bufs.append(S.build_segment(f"nw{i}", cols))
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    for q in ["SELECT g, COUNT(*), SUM(i), SUM(l44), SUM(l60), SUM(dl), AVG(i) FROM t GROUP BY g",
+              "SET numGroupsLimit = 1000000; SELECT a, b, COUNT(*), SUM(i), SUM(l44), SUM(l60) FROM t WHERE g < 40 "
+              "GROUP BY a, b"]:
+        res = engine.ServerQueryExecutor().execute(q, segs)
+        if "GROUP BY a, b" in q:
+            assert res.kernel_info().startswith("jit-partitioned"), res.kernel_info()
+        _, og = oracle.execute(q, bufs)
+        got = res.groups()
+        assert set(got) == set(og)
+        for k in og:
+            assert got[k] == og[k], (q, k, got[k], og[k])
