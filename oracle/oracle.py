@@ -189,6 +189,84 @@ def decompress_chunk(comp: int, src: np.ndarray, dst: np.ndarray, want: int) -> 
     return len(raw)
 
 
+def var_byte_values(cb: ColumnBuffers) -> List[str]:
+    """Every doc's value of a raw STRING forward index, as VarByteChunkForwardIndexReaderV4 / V5 / V6
+    read it (segment/index/readers/forward/VarByteChunkForwardIndexReaderV4.java): BE header, LE chunk
+    metadata (MSB of docIdOffset marks a huge single-value chunk), LE chunks of offsets (V6 with a codec:
+    sizes) and UTF-8 bytes."""
+    import struct
+    b = cb.fwd
+    version, target, comp, chunks_off = struct.unpack_from(">4i", b, 0)
+    assert 4 <= version <= 6, version
+    n = (chunks_off - 16) // 8
+    meta = [struct.unpack_from("<Ii", b, 16 + 8 * k) for k in range(n)]
+    out: List[str] = []
+    for k, (dw, co) in enumerate(meta):
+        s = chunks_off + co
+        e = chunks_off + meta[k + 1][1] if k + 1 < n else len(b)
+        src = np.frombuffer(b[s:e], dtype=np.uint8).copy()
+        if comp == 0:
+            raw = src.tobytes()
+        else:
+            if comp == 4:  # LZ4CompressorWithLength: LE decompressed length first
+                want = int.from_bytes(src[:4].tobytes(), "little")
+                src = src[4:].copy()
+            elif comp == 1:  # snappy varint preamble
+                want, sh, i = 0, 0, 0
+                while True:
+                    want |= (int(src[i]) & 127) << sh
+                    sh += 7
+                    i += 1
+                    if not src[i - 1] & 128:
+                        break
+            elif comp == 5:
+                want = int.from_bytes(src[-4:].tobytes(), "big")
+            elif comp == 2:
+                want = _zstd_content_size(src.tobytes())
+            else:
+                want = 2 * target + 64
+            dst = np.zeros(want + 64, dtype=np.uint8)
+            got = decompress_chunk(comp, src, dst, want)
+            raw = dst[:got].tobytes()
+        if dw & 0x80000000:
+            out.append(raw.decode("utf-8"))
+            continue
+        nd = int.from_bytes(raw[:4], "little")
+        ints = struct.unpack_from("<%di" % nd, raw, 4)
+        if version == 6 and comp != 0:
+            pos = 4 * (nd + 1)
+            for size in ints:
+                out.append(raw[pos:pos + size].decode("utf-8"))
+                pos += size
+        else:
+            for i in range(nd):
+                out.append(raw[ints[i]:ints[i + 1] if i + 1 < nd else len(raw)].decode("utf-8"))
+    assert len(out) == cb.num_docs, (len(out), cb.num_docs)
+    return out
+
+
+def _zstd_content_size(fr: bytes) -> int:
+    """Frame_Content_Size of a zstd frame header (RFC 8878 3.1.1.1)."""
+    d = fr[4]
+    fcs_flag, single, did = d >> 6, (d >> 5) & 1, d & 3
+    pos = 5 + (0 if single else 1) + (0, 1, 2, 4)[did]
+    size = (1 if single else 0, 2, 4, 8)[fcs_flag]
+    v = int.from_bytes(fr[pos:pos + size], "little")
+    return v + 256 if size == 2 else v
+
+
+def _dictionary_twin(cb: ColumnBuffers) -> ColumnBuffers:
+    """ForwardIndexHandler ENABLE_DICTIONARY restated for a raw STRING column: sorted distinct values
+    (String.compareTo order) and a fixed-bit dictId forward index."""
+    from pinot_amd.segment import build_dictionary, dictionary_bytes, num_bits_per_value, pack_fixed_bit
+    vals = np.array(var_byte_values(cb), dtype=object)
+    dvals, ids = build_dictionary(vals, STRING)
+    card = max(len(dvals), 1)
+    bits = num_bits_per_value(card - 1)
+    return ColumnBuffers(cb.name, STRING, cb.num_docs, True, False, card, bits, pack_fixed_bit(ids, bits),
+                         dictionary_bytes(dvals, STRING), None, dvals)
+
+
 def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
     """The contiguous big-endian values of a raw forward index: the data region of PASS_THROUGH
     chunks, or the LZ4 / LZ4_LENGTH_PREFIXED chunks decoded one by one
@@ -218,6 +296,10 @@ class OracleSegment:
     """Host view of one segment's buffers in the oracle's column layout."""
 
     def __init__(self, seg: SegmentBuffers):
+        if any(c.stored_type == STRING and not c.has_dictionary for c in seg.columns.values()):
+            seg = SegmentBuffers(seg.name, seg.num_docs, {
+                n: _dictionary_twin(c) if (c.stored_type == STRING and not c.has_dictionary) else c
+                for n, c in seg.columns.items()})
         self.seg = seg
         self.names = list(seg.columns)
         self.index = {n: i for i, n in enumerate(self.names)}

@@ -209,10 +209,9 @@ static int decode_dictionary(Column& c, const uint8_t* d, size_t n) {
     if (w * (size_t)c.card != n) return fail(PINOT_AMD_EINVAL, "string dictionary size %zu not a multiple of %d", n, c.card);
     c.dict_s.resize(c.card);
     for (int i = 0; i < c.card; ++i) {
+      // FixedByteValueReaderWriter.readUnpaddedBytes: the value ends at its first NUL byte
       const char* p = (const char*)d + (size_t)i * w;
-      size_t len = w;
-      while (len > 0 && p[len - 1] == '\0') --len;
-      c.dict_s[i].assign(p, len);
+      c.dict_s[i].assign(p, strnlen(p, w));
     }
     return 0;
   }
@@ -336,6 +335,201 @@ static const HostCodecs& host_codecs() {
   return hc;
 }
 
+// ---- host chunk decoders for var-byte (STRING) chunks, decoded once at staging ----
+// LZ4 block format (lz4-java LZ4FastDecompressor / LZ4SafeDecompressor, third-party: the published
+// block format): sequences of (token, literals, 2-byte LE offset, match); returns bytes written or -1.
+static int64_t lz4_block_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t cap) {
+  size_t ip = 0, op = 0;
+  while (ip < n) {
+    const uint8_t tok = src[ip++];
+    size_t lit = tok >> 4;
+    if (lit == 15) {
+      uint8_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (ip + lit > n || op + lit > cap) return -1;
+    memcpy(dst + op, src + ip, lit);
+    ip += lit;
+    op += lit;
+    if (ip >= n) break;  // last sequence: literals only
+    if (ip + 2 > n) return -1;
+    const size_t off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    size_t ml = (tok & 15u) + 4;
+    if ((tok & 15u) == 15) {
+      uint8_t b;
+      do {
+        if (ip >= n) return -1;
+        b = src[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    if (op + ml > cap) return -1;
+    for (size_t k = 0; k < ml; ++k, ++op) dst[op] = dst[op - off];  // overlapping copies byte by byte
+  }
+  return (int64_t)op;
+}
+// Snappy raw format (snappy-java, third-party: varint uncompressed length, then literal / copy elements)
+static int64_t snappy_decode(const uint8_t* src, size_t n, std::vector<uint8_t>* out) {
+  size_t ip = 0;
+  uint64_t len = 0;
+  for (int sh = 0; ; sh += 7) {
+    if (ip >= n || sh > 35) return -1;
+    const uint8_t b = src[ip++];
+    len |= (uint64_t)(b & 127u) << sh;
+    if (!(b & 128u)) break;
+  }
+  out->assign(len, 0);
+  uint8_t* dst = out->data();
+  size_t op = 0;
+  while (ip < n) {
+    const uint8_t tag = src[ip++];
+    if ((tag & 3u) == 0) {  // literal
+      size_t l = tag >> 2;
+      if (l >= 60) {
+        const size_t nb = l - 59;
+        if (ip + nb > n) return -1;
+        l = 0;
+        for (size_t k = 0; k < nb; ++k) l |= (size_t)src[ip + k] << (8 * k);
+        ip += nb;
+      }
+      ++l;
+      if (ip + l > n || op + l > len) return -1;
+      memcpy(dst + op, src + ip, l);
+      ip += l;
+      op += l;
+      continue;
+    }
+    size_t l, off;
+    if ((tag & 3u) == 1) {
+      if (ip + 1 > n) return -1;
+      l = ((tag >> 2) & 7u) + 4;
+      off = ((size_t)(tag >> 5) << 8) | src[ip];
+      ip += 1;
+    } else if ((tag & 3u) == 2) {
+      if (ip + 2 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = (size_t)src[ip] | ((size_t)src[ip + 1] << 8);
+      ip += 2;
+    } else {
+      if (ip + 4 > n) return -1;
+      l = (tag >> 2) + 1;
+      off = (size_t)le32(src + ip);
+      ip += 4;
+    }
+    if (off == 0 || off > op || op + l > len) return -1;
+    for (size_t k = 0; k < l; ++k, ++op) dst[op] = dst[op - off];
+  }
+  return op == len ? (int64_t)len : -1;
+}
+
+// One var-byte chunk decompressed on the host (ChunkCompressorFactory.getDecompressor per
+// ChunkCompressionType: PASS_THROUGH, SNAPPY, ZSTANDARD, LZ4, LZ4_LENGTH_PREFIXED, GZIP).
+static int decode_var_chunk(int comp, const uint8_t* src, size_t n, size_t target, std::vector<uint8_t>* out) {
+  switch (comp) {
+    case 0: out->assign(src, src + n); return 0;
+    case 1: return snappy_decode(src, n, out) < 0 ? -1 : 0;
+    case 2: {
+      const HostCodecs& hc = host_codecs();
+      if (!hc.zstd_decompress) return -2;
+      out->assign(std::max<size_t>(target, 1) * 2 + 64, 0);
+      size_t got = hc.zstd_decompress(out->data(), out->size(), src, n);
+      if (hc.zstd_is_error(got)) return -1;
+      out->resize(got);
+      return 0;
+    }
+    case 3:
+    case 4: {
+      // LZ4CompressorWithLength: 4-byte LE decompressed length, then the block (V4+ writers always
+      // upgrade LZ4 to the length-prefixed form; a bare LZ4 block is bounded by the chunk target size)
+      size_t want, off = 0;
+      if (comp == 4) {
+        if (n < 4) return -1;
+        want = le32(src);
+        off = 4;
+      } else {
+        want = std::max<size_t>(target, 1) * 2 + 64;
+      }
+      out->assign(want, 0);
+      const int64_t got = lz4_block_decode(src + off, n - off, out->data(), want);
+      if (got < 0 || (comp == 4 && (size_t)got != want)) return -1;
+      out->resize((size_t)got);
+      return 0;
+    }
+    case 5: {
+      const HostCodecs& hc = host_codecs();
+      if (!hc.z_uncompress) return -2;
+      if (n < 4) return -1;
+      unsigned long dl = be32(src + n - 4);
+      out->assign(dl, 0);
+      if (hc.z_uncompress(out->data(), &dl, src, n - 4) != 0) return -1;
+      out->resize(dl);
+      return 0;
+    }
+    default: return -2;
+  }
+}
+
+// Raw STRING forward index (VarByteChunkForwardIndexReaderV4 / V5 / V6: BE header {version,
+// targetDecompressedChunkSize, ChunkCompressionType, chunksOffset}, LE metadata {docIdOffset | huge
+// bit, chunkOffset} per chunk, LE chunks {numDocs, per-doc offsets (V6 compressed: sizes), bytes}; a
+// huge chunk is one value). Decoded into per-doc strings.
+static int read_var_byte_strings(const char* name, const uint8_t* fwd, size_t size, int64_t num_docs,
+                                 std::vector<std::string>* vals) {
+  if (size < 16) return fail(PINOT_AMD_EINVAL, "column %s: var-byte header truncated", name);
+  const int32_t version = (int32_t)be32(fwd), target = (int32_t)be32(fwd + 4), comp = (int32_t)be32(fwd + 8);
+  const uint32_t chunks_off = be32(fwd + 12);
+  if (version < 4 || version > 6)
+    return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw STRING forward index version %d", name, version);
+  if (chunks_off < 16 || chunks_off > size || (chunks_off - 16) % 8 != 0)
+    return fail(PINOT_AMD_EINVAL, "column %s: bad var-byte metadata", name);
+  const size_t nchunks = (chunks_off - 16) / 8;
+  vals->clear();
+  vals->reserve((size_t)num_docs);
+  std::vector<uint8_t> buf;
+  for (size_t k = 0; k < nchunks; ++k) {
+    const uint32_t doc_word = le32(fwd + 16 + 8 * k);
+    const bool huge = (doc_word & 0x80000000u) != 0;
+    const uint64_t s = (uint64_t)chunks_off + le32(fwd + 16 + 8 * k + 4);
+    const uint64_t e = k + 1 < nchunks ? (uint64_t)chunks_off + le32(fwd + 16 + 8 * (k + 1) + 4) : size;
+    if (s > e || e > size || (doc_word & 0x7FFFFFFFu) != vals->size())
+      return fail(PINOT_AMD_EINVAL, "column %s: bad var-byte chunk %zu", name, k);
+    const int rc = decode_var_chunk(comp, fwd + s, (size_t)(e - s), (size_t)target, &buf);
+    if (rc == -2) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: chunk compression %d", name, comp);
+    if (rc) return fail(PINOT_AMD_EINVAL, "column %s: var-byte chunk %zu does not decode", name, k);
+    if (huge) {
+      vals->emplace_back((const char*)buf.data(), buf.size());
+      continue;
+    }
+    if (buf.size() < 4) return fail(PINOT_AMD_EINVAL, "column %s: empty var-byte chunk %zu", name, k);
+    const uint32_t nd = le32(buf.data());
+    if ((uint64_t)4 * (nd + 1) > buf.size()) return fail(PINOT_AMD_EINVAL, "column %s: var-byte chunk %zu header", name, k);
+    const bool sizes = version == 6 && comp != 0;  // VarByteChunkForwardIndexWriterV6: delta-encoded offsets
+    uint64_t pos = 4ull * (nd + 1);
+    for (uint32_t i = 0; i < nd; ++i) {
+      uint64_t a, b;
+      if (sizes) {
+        a = pos;
+        b = a + le32(buf.data() + 4 + 4 * i);
+      } else {
+        a = le32(buf.data() + 4 + 4 * i);
+        b = i + 1 < nd ? le32(buf.data() + 8 + 4 * i) : buf.size();
+      }
+      if (a > b || b > buf.size()) return fail(PINOT_AMD_EINVAL, "column %s: var-byte value bounds in chunk %zu", name, k);
+      vals->emplace_back((const char*)buf.data() + a, (size_t)(b - a));
+      pos = b;
+    }
+  }
+  if ((int64_t)vals->size() != num_docs)
+    return fail(PINOT_AMD_EINVAL, "column %s: var-byte index holds %zu of %lld docs", name, vals->size(), (long long)num_docs);
+  return 0;
+}
+
 // Stage a raw forward index with compressed chunks (BaseChunkForwardIndexReader.java:60-105,150-185;
 // codecs per ChunkCompressionType.java:22): LZ4, LZ4_LENGTH_PREFIXED, SNAPPY, DELTA and DELTADELTA
 // chunks are decoded on the device (chunk_decompress_kernel, one wave per chunk) straight into the
@@ -449,6 +643,50 @@ const void* pinot_amd_segment_column_fwd(const pinot_amd_segment* seg, const cha
 int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_spec* spec) {
   if (!seg || !spec || !spec->name) return fail(PINOT_AMD_EINVAL, "add_column: bad arguments");
   if (seg->cols.count(spec->name)) return fail(PINOT_AMD_EINVAL, "add_column: duplicate column %s", spec->name);
+  if (spec->encoding == ENC_RAW && spec->stored_type == T_STRING) {
+    // Raw STRING column: staged dictionary-encoded, as ForwardIndexHandler's ENABLE_DICTIONARY operation
+    // rewrites it on load (segment/index/loader/ForwardIndexHandler.java): the distinct values sorted in
+    // String.compareTo order (the StringDictionary order), dictIds in a fixed-bit forward index. Every
+    // predicate and GROUP BY then runs through the dictionary path with the same docIds and values as
+    // the raw-value evaluators. A legacy raw-value inverted index is dropped, as
+    // SegmentPreProcessor.removeLegacyRawValueInvertedIndexes does; the scan path covers its predicates.
+    if (!spec->h_fwd) return fail(PINOT_AMD_EINVAL, "column %s: no forward index", spec->name);
+    std::vector<std::string> vals;
+    if (int rc = read_var_byte_strings(spec->name, (const uint8_t*)spec->h_fwd, spec->fwd_size, seg->num_docs, &vals))
+      return rc;
+    std::vector<std::string> uniq(vals);
+    std::sort(uniq.begin(), uniq.end(), java_less);
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    const int32_t card = (int32_t)std::max<size_t>(uniq.size(), 1);
+    int bits = 1;
+    while ((1ll << bits) < (int64_t)card) ++bits;  // PinotDataBitSet.getNumBitsPerValue(card - 1)
+    size_t width = 1;
+    for (auto& u : uniq) width = std::max(width, u.size());
+    std::vector<uint8_t> dict((size_t)card * width, 0);
+    for (size_t i = 0; i < uniq.size(); ++i) memcpy(&dict[i * width], uniq[i].data(), uniq[i].size());
+    std::vector<uint8_t> fb((size_t)((seg->num_docs * bits + 7) / 8) + 8, 0);
+    uint64_t acc = 0;
+    int nacc = 0;
+    size_t o = 0;
+    for (const std::string& v : vals) {
+      const uint64_t id = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), v, java_less) - uniq.begin());
+      acc = (acc << bits) | id;
+      nacc += bits;
+      while (nacc >= 8) { fb[o++] = (uint8_t)(acc >> (nacc - 8)); nacc -= 8; }
+    }
+    if (nacc > 0) fb[o++] = (uint8_t)(acc << (8 - nacc));
+    pinot_amd_column_spec d = *spec;
+    d.encoding = ENC_FIXED_BIT;
+    d.cardinality = card;
+    d.bits_per_element = bits;
+    d.h_fwd = fb.data();
+    d.fwd_size = fb.size();
+    d.h_dictionary = dict.data();
+    d.dictionary_size = dict.size();
+    d.h_inverted = nullptr;
+    d.inverted_size = 0;
+    return pinot_amd_segment_add_column(seg, &d);
+  }
   auto c = std::make_unique<Column>();
   c->name = spec->name;
   c->type = spec->stored_type;
@@ -481,12 +719,16 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
     }
     case ENC_RAW: {
       if (c->type == T_STRING) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw STRING", spec->name);
-      if (spec->fwd_size < 28) return fail(PINOT_AMD_EINVAL, "column %s: raw index header truncated", spec->name);
-      // BaseChunkForwardIndexReader.java:60-105
+      if (spec->fwd_size < 16) return fail(PINOT_AMD_EINVAL, "column %s: raw index header truncated", spec->name);
+      // BaseChunkForwardIndexReader.java:60-105: version 1 files have a 16-byte header and SNAPPY
+      // chunks; later versions add total docs, the ChunkCompressionType and the data header start
       const int32_t version = (int32_t)be32(fwd), num_chunks = (int32_t)be32(fwd + 4);
       const int32_t size = (int32_t)be32(fwd + 12);
-      if (version < 2) return fail(PINOT_AMD_EUNSUPPORTED, "column %s: raw index v%d (SNAPPY)", spec->name, version);
-      const int32_t comp = (int32_t)be32(fwd + 20), dhs = (int32_t)be32(fwd + 24);
+      if (version < 1) return fail(PINOT_AMD_EINVAL, "column %s: raw index version %d", spec->name, version);
+      if (version > 1 && spec->fwd_size < 28)
+        return fail(PINOT_AMD_EINVAL, "column %s: raw index header truncated", spec->name);
+      const int32_t comp = version > 1 ? (int32_t)be32(fwd + 20) : 1 /* SNAPPY */;
+      const int32_t dhs = version > 1 ? (int32_t)be32(fwd + 24) : 16;
       if (size != value_size(c->type)) return fail(PINOT_AMD_EINVAL, "column %s: entry size %d", spec->name, size);
       const size_t off_size = version <= 2 ? 4 : 8;
       const size_t raw_start = (size_t)dhs + (size_t)num_chunks * off_size;

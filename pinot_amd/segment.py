@@ -247,6 +247,52 @@ def chunk_compress(raw: bytes, compression: int) -> bytes:
     raise NotImplementedError(f"compression {compression}")
 
 
+def var_byte_fwd_bytes(values, version: int = 4, compression: int = PASS_THROUGH, chunk_size: int = 4096) -> bytes:
+    """Raw STRING forward index as VarByteChunkForwardIndexWriterV4 / V5 / V6 write it
+    (io/writer/impl/VarByteChunkForwardIndexWriterV4.java): BE header {version, target chunk size,
+    compression, chunks offset}; LE metadata {docIdOffset (MSB: huge chunk), chunk offset} per chunk;
+    LE chunks {numDocs, offsets (V6 with compression: sizes), UTF-8 bytes}; a value that does not fit
+    a chunk is written alone as a huge chunk. LZ4 is upgraded to LZ4_LENGTH_PREFIXED like the writer."""
+    comp = LZ4_LENGTH_PREFIXED if compression == LZ4 else compression
+    meta, data = [], bytearray()
+    cur: list = []
+    state = {"pos": 4, "doc_off": 0, "next": 0}
+
+    def write(buf: bytes, huge: bool):
+        c = chunk_compress(buf, comp) if comp != PASS_THROUGH else buf
+        meta.append((state["doc_off"] | (0x80000000 if huge else 0), len(data)))
+        data.extend(c)
+        state["doc_off"] = state["next"]
+
+    def flush():
+        if not cur:
+            return
+        nd = len(cur)
+        offs = [4 * (nd + 1)]
+        for v in cur[:-1]:
+            offs.append(offs[-1] + len(v))
+        ints = [len(v) for v in cur] if (version == 6 and comp != PASS_THROUGH) else offs
+        write(struct.pack("<%di" % (nd + 1), nd, *ints) + b"".join(cur), False)
+        cur.clear()
+        state["pos"] = 4
+
+    for s in values:
+        b = s.encode("utf-8")
+        need = 4 + len(b)
+        if state["pos"] > chunk_size - need:
+            flush()
+            if need > chunk_size - 4:
+                state["next"] += 1
+                write(b, True)
+                continue
+        cur.append(b)
+        state["pos"] += need
+        state["next"] += 1
+    flush()
+    hdr = struct.pack(">4i", version, chunk_size, comp, 16 + 8 * len(meta))
+    return hdr + b"".join(struct.pack("<Ii", d, o) for d, o in meta) + bytes(data)
+
+
 def raw_fwd_header(n: int, stored_type: str, version: int = 4, docs_per_chunk: int = 1000) -> bytes:
     """Header + chunk-offset table of a PASS_THROUGH FixedByteChunkForwardIndexWriter file of n values."""
     if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
@@ -298,7 +344,8 @@ def dictionary_bytes(sorted_values, stored_type: str) -> bytes:
 def decode_dictionary(buf: bytes, stored_type: str, cardinality: int) -> np.ndarray:
     if stored_type == STRING:
         width = len(buf) // max(cardinality, 1)
-        return np.array([buf[i * width:(i + 1) * width].rstrip(b"\0").decode("utf-8") for i in range(cardinality)],
+        # FixedByteValueReaderWriter.readUnpaddedBytes: a value ends at its first NUL byte
+        return np.array([buf[i * width:(i + 1) * width].split(b"\0", 1)[0].decode("utf-8") for i in range(cardinality)],
                         dtype=object)
     return np.frombuffer(buf, dtype=_NP_BE[stored_type], count=cardinality).astype(_NP_LE[stored_type])
 
@@ -494,7 +541,8 @@ def build_column(name: str, values, stored_type: str, dictionary: bool = True, i
     n = int(vals.size)
     if not dictionary:
         if stored_type == STRING:
-            raise NotImplementedError("raw STRING forward index is outside the hot path")
+            return ColumnBuffers(name, stored_type, n, False,
+                                 fwd=var_byte_fwd_bytes([str(v) for v in vals], max(raw_version, 4), compression))
         return ColumnBuffers(name, stored_type, n, False,
                              fwd=raw_fwd_bytes(vals, stored_type, raw_version, compression=compression))
     dvals, ids = build_dictionary(vals, stored_type)
@@ -521,3 +569,84 @@ def build_segment(name: str, columns: Dict[str, tuple]) -> SegmentBuffers:
             raise ValueError("ragged columns")
         cols[cname] = c
     return SegmentBuffers(name, n or 0, cols)
+
+
+# --------------------------------------------------------------------------- segment directories
+V3_MAGIC_MARKER = 0xDEADBEEFDEAFBEAD  # SingleFileIndexDirectory.java:79, written before every index
+
+
+def read_properties(path: str) -> Dict[str, str]:
+    """metadata.properties / index_map (java.util.Properties key = value lines; \\uXXXX escapes)."""
+    out = {}
+    with open(path, encoding="latin-1") as f:
+        for line in f:
+            line = line.strip()
+            if not line or line[0] in "#!" or "=" not in line:
+                continue
+            k, v = line.split("=", 1)
+            out[k.strip()] = v.strip().encode("latin-1").decode("unicode_escape")
+    return out
+
+
+_V1_FWD_SUFFIX = {"sorted": ".sv.sorted.fwd", "unsorted": ".sv.unsorted.fwd", "raw": ".sv.raw.fwd"}
+_TYPE_NAMES = {"INT": INT, "LONG": LONG, "FLOAT": FLOAT, "DOUBLE": DOUBLE, "STRING": STRING}
+
+
+def load_segment_dir(path: str) -> SegmentBuffers:
+    """Read an immutable segment directory the way ImmutableSegmentLoader / SegmentDirectory map it
+    (pinot-segment-local/.../segment/store/SegmentLocalFSDirectory.java): metadata.properties for the
+    column metadata; index buffers from V1 per-index files (FilePerIndexDirectory: <col>.dict,
+    <col>.sv.{sorted,unsorted,raw}.fwd, <col>.bitmap.inv) or from V3's single columns.psf sliced by
+    index_map (SingleFileIndexDirectory: <col>.<index>.startOffset / .size, each index prefixed by an
+    8-byte magic marker). Single-value INT / LONG / FLOAT / DOUBLE / STRING columns; a raw column's
+    legacy raw-value inverted index is dropped (SegmentPreProcessor.removeLegacyRawValueInvertedIndexes)."""
+    import os
+    v3 = os.path.join(path, "v3")
+    if os.path.isdir(v3):
+        path = v3
+    meta = read_properties(os.path.join(path, "metadata.properties"))
+    num_docs = int(meta["segment.total.docs"])
+    cols = sorted({k.split(".")[1] for k in meta if k.startswith("column.") and k.count(".") >= 2})
+    psf = None
+    index_map = {}
+    if os.path.exists(os.path.join(path, "index_map")):
+        index_map = read_properties(os.path.join(path, "index_map"))
+        with open(os.path.join(path, "columns.psf"), "rb") as f:
+            psf = f.read()
+
+    def index_bytes(col: str, index: str, v1_suffix: str) -> Optional[bytes]:
+        if psf is not None:
+            k = f"{col}.{index}.startOffset"
+            if k not in index_map:
+                return None
+            off, size = int(index_map[k]), int(index_map[f"{col}.{index}.size"])
+            marker = int.from_bytes(psf[off:off + 8], "big")
+            if marker != V3_MAGIC_MARKER:
+                raise ValueError(f"{col}.{index}: bad magic marker {marker:#x}")
+            return psf[off + 8:off + size]
+        fn = os.path.join(path, col + v1_suffix)
+        if not os.path.exists(fn):
+            return None
+        with open(fn, "rb") as f:
+            return f.read()
+
+    out = {}
+    for c in cols:
+        m = {k[len("column.") + len(c) + 1:]: v for k, v in meta.items() if k.startswith(f"column.{c}.")}
+        if m.get("isSingleValues", "true") != "true":
+            raise NotImplementedError(f"multi-value column {c}")
+        st = _TYPE_NAMES[m["dataType"]]
+        has_dict = m.get("hasDictionary", "true") == "true"
+        is_sorted = m.get("isSorted", "false") == "true"
+        card = int(m.get("cardinality", "0"))
+        bits = int(m.get("bitsPerElement", "0"))
+        if not has_dict:
+            fwd = index_bytes(c, "forward_index", _V1_FWD_SUFFIX["raw"])
+            out[c] = ColumnBuffers(c, st, num_docs, False, fwd=fwd)
+            continue
+        fwd = index_bytes(c, "forward_index", _V1_FWD_SUFFIX["sorted" if is_sorted else "unsorted"])
+        dic = index_bytes(c, "dictionary", ".dict")
+        inv = index_bytes(c, "inverted_index", ".bitmap.inv")
+        out[c] = ColumnBuffers(c, st, num_docs, True, is_sorted, card, bits, fwd, dic, inv,
+                               decode_dictionary(dic, st, card))
+    return SegmentBuffers(meta.get("segment.name", os.path.basename(path)), num_docs, out)
