@@ -232,18 +232,17 @@ int pinot_amd_result_destroy(pinot_amd_result* r);
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out);
 /* Number of groups with >= 1 matching doc (1 for an aggregation-only query). */
 int pinot_amd_result_num_groups(pinot_amd_result* r, int64_t* h_out);
-/* numGroupsLimitReached (DefaultGroupByExecutor / GroupByResultsBlock metadata): 1 when the merged
- * result holds more groups than the query's numGroupsLimit. Pinot drops the groups a segment first
- * sees after its limit is reached (DictionaryBasedGroupKeyGenerator.java:352-360, first-seen docId
- * order); this library keeps every group, so its results equal Pinot's exactly when this is 0 —
- * set the numGroupsLimit query option above the expected group count for high-cardinality GROUP BY.
- * Conservative: the merged count bounds every segment's count. */
+/* numGroupsLimitReached (GroupByOperator / GroupByResultsBlock metadata): 1 when some segment reached
+ * the query's numGroupsLimit. As in Pinot, each segment admits only the first numGroupsLimit groups
+ * it sees in docId order (DictionaryBasedGroupKeyGenerator.java:351-363); later groups of that
+ * segment are dropped, and the combine keeps the union of the admitted groups. */
 int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_out);
 /* Fetch up to cap groups: h_keys[g*num_group_by + j] = group-by column j's value as int64 (INT/LONG),
  * its double bits (FLOAT/DOUBLE) or its index into the merged STRING dictionary
  * (pinot_amd_result_string_key); h_values[g*num_aggs + a] = final result as double
- * (COUNT, SUM, MIN, MAX, AVG, SUMLONG as double); h_values_i64 (optional) = exact COUNT / SUM on
- * integer columns / SUMLONG. Groups are ordered by ascending global key. */
+ * (COUNT, SUM, MIN, MAX, AVG, SUMLONG, MINMAXRANGE as double; SUM of integers is the exact 128-bit
+ * sum rounded once); h_values_i64 (optional) = exact COUNT / SUMLONG, and SUM on integer columns when
+ * it fits int64 (INT64_MIN otherwise). Groups are ordered by ascending global key. */
 int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, double* h_values,
                            int64_t* h_values_i64, int64_t* h_num_fetched);
 /* AggregationFunction.extractAggregationResult: the intermediate result of every aggregation, two
@@ -255,7 +254,8 @@ int pinot_amd_result_fetch_intermediate(pinot_amd_result* r, int64_t cap, double
 const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t id);
 /* Device view of the dense accumulators for a multi-GPU merge (RCCL all-reduce in place):
  * per aggregation slot an array of num_key_slots 8-byte words; op per slot: 0 = sum(int64),
- * 1 = sum(double), 2 = min(uint64 ordered), 3 = max(uint64 ordered). */
+ * 1 = sum(double), 2 = min(uint64 ordered), 3 = max(uint64 ordered), 4 / 5 = low / high word of an
+ * exact 128-bit integer sum. EUNSUPPORTED for hash-table plans (merge those by value). */
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops);
 /* Which scan kernel the plan runs: "jit" (query-specialised, compiled with hipRTC) or
