@@ -2045,8 +2045,54 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   base.num_keys = num_keys;
   base.bitset = filter_only;
   base.aggregate = q.nacc > 0;
-  const int64_t lds_bytes = (int64_t)q.nacc * std::max<int64_t>(num_keys, 1) * 8;
+  int cus = 256;
+  {
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  // Integer SUMs into an LDS table keep 64-bit partials (no high word in LDS) when |value| x (docs one
+  // block adds) < 2^63 for every segment: a scan block owns ceil(tiles / grid) tiles with grid >=
+  // min(CUs, tiles / kPartSub); a partition aggregation block ceil(records / agg_grid) <= ceil(docs /
+  // CUs) records. Bounded with the whole batch, so every launch of the plan satisfies it.
+  int64_t all_tiles = 0, all_docs = 0;
+  for (auto* s : segs) {
+    all_tiles += (s->num_docs + kTileDocs - 1) / kTileDocs;
+    all_docs += s->num_docs;
+  }
+  auto set_narrow = [&](__int128 docs_bound) {
+    auto maxabs = [&](int sl) -> __int128 {
+      __int128 m = 0;
+      for (auto* s : segs) {
+        const Column& c = *s->cols.at(slot_cols[sl]);
+        if (!c.has_range) return -1;
+        const __int128 a = c.vmax < 0 ? -(__int128)c.vmax : (__int128)c.vmax;
+        const __int128 b = c.vmin < 0 ? -(__int128)c.vmin : (__int128)c.vmin;
+        m = std::max(m, std::max(a, b));
+      }
+      return m;
+    };
+    for (JitAcc& a : base.accs) {
+      a.narrow = 0;
+      if (a.op != ACC_SUM_I128 || env_is("PINOT_AMD_NARROW_SUMS", "0")) continue;
+      __int128 m = maxabs(a.slot);
+      if (m >= 0 && a.expr != EXPR_COL) {
+        const __int128 m2 = maxabs(a.slot2);
+        m = m2 < 0 ? -1 : a.expr == EXPR_MUL ? m * m2 : m + m2;
+      }
+      a.narrow = (m >= 0 && m * docs_bound <= (__int128)INT64_MAX) ? 1 : 0;
+    }
+  };
+  auto lds_arrays = [&]() {
+    int k = 0;
+    jit_lds_layout(base, &k);
+    return (int64_t)k;
+  };
+  int64_t lds_bytes = (int64_t)q.nacc * std::max<int64_t>(num_keys, 1) * 8;
   if (r->kind == PLAN_DENSE && q.nacc > 0) {
+    const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
+    set_narrow((__int128)((all_tiles + min_grid - 1) / min_grid) * kTileDocs);
+    lds_bytes = lds_arrays() * std::max<int64_t>(num_keys, 1) * 8;
     if (lds_bytes <= 40 * 1024) {  // LDS-privatised table, four 256-thread blocks per CU
       base.lds = true;
     } else if (lds_bytes <= lds_max && !env_is("PINOT_AMD_WIDE_LDS", "0")) {
@@ -2055,10 +2101,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     } else if (!env_is("PINOT_AMD_PARTITIONED", "0") && !Q.group_by.empty()) {
       // key space too large for an LDS table: partition the matching docs by key range and aggregate
       // each partition in LDS (random per-lane HBM atomics run ~17x below the coalesced rate)
+      set_narrow((__int128)((all_docs + cus - 1) / cus));
+      const int64_t na = lds_arrays();
       int shift = 16;
-      while (shift > 6 && (int64_t)q.nacc * ((int64_t)1 << shift) * 8 > lds_max) --shift;
+      while (shift > 6 && na * ((int64_t)1 << shift) * 8 > lds_max) --shift;
       const int64_t nparts = (num_keys + ((int64_t)1 << shift) - 1) >> shift;
-      if ((int64_t)q.nacc * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
+      if (na * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
         r->kind = PLAN_PARTITIONED;
         base.partitioned = true;
         base.key_shift = shift;
@@ -2070,6 +2118,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
     }
   }
+  if (!base.lds && !base.partitioned)
+    for (JitAcc& a : base.accs) a.narrow = 0;  // HBM tables take full 128-bit adds
   if (r->kind == PLAN_HASH) {
     base.hash = true;
     base.hash_seg = r->trim;
@@ -2078,9 +2128,6 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
 
   // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
-  int dev = 0, cus = 256;
-  HIP_OK(hipGetDevice(&dev));
-  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
   std::vector<int32_t> key_seg(n, 0);
   {
@@ -2180,33 +2227,6 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
       jp.leaves.push_back(jl);
     }
-    if ((jp.lds || jp.partitioned) && !env_is("PINOT_AMD_NARROW_SUMS", "0")) {
-      // integer SUMs into an LDS table: 64-bit partials when |value| x (docs one block adds) < 2^63.
-      // Scan blocks own ceil(tiles / grid) tiles and grid >= min(CUs, tiles / kPartSub); a partition
-      // aggregation block takes ceil(records / agg_grid) <= ceil(docs / CUs) records.
-      const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, tiles / kPartSub));
-      const __int128 docs_bound = jp.partitioned ? (__int128)((L.docs + cus - 1) / cus)
-                                                 : (__int128)((tiles + min_grid - 1) / min_grid) * kTileDocs;
-      auto maxabs = [&](int sl) -> __int128 {  // over the launch's segments; -1: unknown
-        __int128 m = 0;
-        for (int si : L.segs) {
-          const Column& c = *segs[si]->cols.at(slot_cols[sl]);
-          if (!c.has_range) return -1;
-          m = std::max(m, std::max((__int128)c.vmax < 0 ? -(__int128)c.vmax : (__int128)c.vmax,
-                                   (__int128)c.vmin < 0 ? -(__int128)c.vmin : (__int128)c.vmin));
-        }
-        return m;
-      };
-      for (JitAcc& a : jp.accs) {
-        if (a.op != ACC_SUM_I128) continue;
-        __int128 m = maxabs(a.slot);
-        if (m >= 0 && a.expr != EXPR_COL) {
-          const __int128 m2 = maxabs(a.slot2);
-          m = m2 < 0 ? -1 : a.expr == EXPR_MUL ? m * m2 : m + m2;
-        }
-        a.narrow = (m >= 0 && m * docs_bound <= (__int128)INT64_MAX) ? 1 : 0;
-      }
-    }
     {  // pipeline depth: ~4 KiB in flight per wave (256 docs x bytes per row)
       double bpr = 0;
       for (const JitSlot& js : jp.slots)
@@ -2278,7 +2298,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.part.nparts = jp.nparts;
       L.part.key_shift = jp.key_shift;
       L.shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
-      L.shmem_agg = (size_t)q.nacc * ((size_t)1 << jp.key_shift) * 8;
+      L.shmem_agg = (size_t)lds_arrays() * ((size_t)1 << jp.key_shift) * 8;
       L.shmem = (size_t)jp.nparts * 4;
       max_rec = std::max(max_rec, (size_t)L.docs * jp.rec_bytes + 256);
       int nb = 0;

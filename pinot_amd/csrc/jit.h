@@ -85,6 +85,9 @@ struct JitPlan {
 void jit_layout_records(JitPlan* p);
 // LDS bytes of the scatter pass for a staging capacity
 size_t jit_scatter_lds(const JitPlan& p, int cap);
+// LDS-privatised table layout: accumulator -> LDS array (-1: the high word of a narrow 128-bit sum,
+// kept only in HBM); *narrays = arrays the LDS table holds
+std::vector<int> jit_lds_layout(const JitPlan& p, int* narrays);
 struct JitKernel {
   std::vector<char> image;
   hipModule_t module = nullptr;

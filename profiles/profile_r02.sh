@@ -34,3 +34,6 @@ for w in ${WORKLOADS:-scan highcard inv0 inv3 ssb3 ssb6}; do
     echo "$w pmc$i done"
   done
 done
+# summarise on the box and drop the raw traces (gpurun copies back at most 64 MiB)
+python3 profiles/summarize_r02.py $OUT gpurun_out/prof2_summary > /dev/null && \
+  find $OUT -name "run_kernel_trace.csv" -o -name "run_counter_collection.csv" | xargs rm -f
