@@ -1797,6 +1797,23 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       seg_bound[si] = (int64_t)b;
       limit_possible |= seg_bound[si] >= Q.num_groups_limit;
     }
+    // The key space alone allows numGroupsLimit groups somewhere: bound each segment by its matching
+    // docs too (a segment's groups <= its matching docs). Counted once at plan time by a filter-only
+    // pass; segments are immutable, so the counts hold for every re-execution of the plan.
+    if (limit_possible && !Q.preds.empty() && !env_is("PINOT_AMD_TRIM_PROBE", "0")) {
+      pinot_amd_query fq;
+      fq.preds = Q.preds;
+      pinot_amd_result* fr = nullptr;
+      if (int rc = execute_impl(&fq, segs.data(), n, stream, true, &fr)) return rc;
+      std::unique_ptr<pinot_amd_result> hold(fr);
+      limit_possible = false;
+      for (int si = 0; si < n; ++si) {
+        int64_t cnt = 0;
+        if (int rc = pinot_amd_bitset_count((const uint64_t*)fr->bitsets[si]->p, segs[si]->num_docs, &cnt, stream)) return rc;
+        seg_bound[si] = std::min(seg_bound[si], cnt);
+        limit_possible |= seg_bound[si] >= Q.num_groups_limit;
+      }
+    }
   }
   r->limit_possible = limit_possible;
 
