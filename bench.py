@@ -251,11 +251,13 @@ def main():
         # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
         # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
         traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", "r01", "pmc_summary_bench40seg.json")
-        if os.path.exists(pmc) and res.kernel_info() == "jit" and args.workload == "scan":
-            d = json.load(open(pmc))["derived"]
-            traffic = (d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]) / d["rows_per_launch"] * rows_per_rank
-            traffic_src = "profiles/r01/pmc_summary_bench40seg.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-row)"
+        pmc = os.path.join(ROOT, "profiles", "r02", "pmc_index.json")
+        if os.path.exists(pmc) and args.workload == "scan" and args.query_index is None:
+            d = json.load(open(pmc)).get("scan")
+            if d and d["query"] == query:
+                traffic = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows_per_rank
+                traffic_src = ("profiles/r02/pmc_index.json (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE per execution "
+                               "of this query over 40 segments, scaled per row; profiles/profile_r02.sh)")
 
         if rank == 0:
             cpu = None
