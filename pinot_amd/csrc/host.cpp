@@ -1892,7 +1892,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   // dense table: mixed-radix keys over the merged dictionaries; hash table: key spaces beyond the
   // dense cap (DictionaryBasedGroupKeyGenerator's Int/Long/ArrayMapBasedHolder) and numGroupsLimit
   // trimming (keys admitted per segment in first-seen order)
-  const int64_t dense_cap = env_i64("PINOT_AMD_DENSE_MAX_KEYS", (int64_t)1 << 28);
+  // dense keys are 32-bit in the kernels (K[4]): never above 2^31, whatever the override says
+  const int64_t dense_cap = std::min<int64_t>(env_i64("PINOT_AMD_DENSE_MAX_KEYS", (int64_t)1 << 28), (int64_t)1 << 31);
   if (filter_only) {
     r->kind = PLAN_FILTER;
   } else if (Q.group_by.empty()) {
