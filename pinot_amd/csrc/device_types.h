@@ -135,6 +135,12 @@ struct DevQuery {
   int32_t acc_op[kMaxAcc];
   int64_t num_keys;                         // dense key space (1 for aggregation only; hash plans: 0)
   int64_t total_tiles;                      // 1024-doc tiles of this launch
+  // selection-vector plans (late materialisation): the filter pass appends (segment << 32 | docId)
+  // entries, each wave's run padded to a multiple of 4 with docId 0xFFFFFFFF; the gather pass
+  // aggregates them. sel_count[0] = entries appended, sel_count[1] = runs that did not fit sel_cap
+  unsigned long long* sel_entries;
+  unsigned long long* sel_count;
+  int64_t sel_cap;
 };
 
 }  // namespace pamd

@@ -1056,6 +1056,10 @@ struct Launch {
   int64_t docs = 0, tiles = 0;
   double col_bytes = 0;  // algorithmic bytes of the launch's decoded columns over all its docs
   bool gated = false;    // an inverted-index gate clause: columns are read only where it passes
+  // selection-vector plan (late materialisation): select pass over the filter columns, gather pass
+  bool select = false;
+  int gather_grid = 1, gather_threads = 256;
+  double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
 };
 
 enum PlanKind { PLAN_DENSE = 0, PLAN_PARTITIONED = 1, PLAN_HASH = 2, PLAN_FILTER = 3 };
@@ -1096,6 +1100,8 @@ struct pinot_amd_result {
   std::string jit_status;
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
+  // selection-vector plans: the shared vector (launches run one after another) and 2 counters per launch
+  DevBuf sel, sel_ctr;
   // hash-table GROUP BY
   int nw = 0;                          // key words (group columns)
   std::vector<int> pack_word, pack_shift, pack_bits;
@@ -1549,6 +1555,29 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   unsigned long long* matched = (unsigned long long*)r->matched.p + 3 * li;
   DevHash h = H;
   void* args[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
+  if (L.select) {  // select pass (filter columns -> selection vector), then the gather-aggregate pass
+    HIP_OK(hipMemsetAsync(L.q.sel_count, 0, 16, st));
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+    if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
+      unsigned long long ctr[2];
+      HIP_OK(hipMemcpyAsync(ctr, L.q.sel_count, 16, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      if (ctr[1] != 0 || ctr[0] > (unsigned long long)L.q.sel_cap || ctr[0] % 4 != 0)
+        return fail(PINOT_AMD_EINVAL, "select check: count %llu overflow %llu cap %lld", ctr[0], ctr[1], (long long)L.q.sel_cap);
+      std::vector<unsigned long long> ent(ctr[0]);
+      if (!ent.empty()) HIP_OK(hipMemcpy(ent.data(), L.q.sel_entries, ent.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<DevSegment> ds(L.segs.size());
+      HIP_OK(hipMemcpy(ds.data(), L.d_segs.p, ds.size() * sizeof(DevSegment), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < ent.size(); ++i) {
+        const uint32_t sg = (uint32_t)(ent[i] >> 32), d = (uint32_t)ent[i];
+        if (sg >= ds.size() || (d != 0xFFFFFFFFu && (int64_t)d >= ds[sg].num_docs) || (uint32_t)(ent[i & ~(size_t)3] >> 32) != sg)
+          return fail(PINOT_AMD_EINVAL, "select check: entry %zu = seg %u doc %u (segments %zu)", i, sg, d, ds.size());
+      }
+    }
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn_gather, (unsigned)L.gather_grid, 1, 1, (unsigned)L.gather_threads, 1, 1,
+                                 (unsigned)L.shmem, st, args, nullptr));
+    return 0;
+  }
   if (r->kind != PLAN_PARTITIONED) {
     HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock * L.scan_nsub, 1, 1, (unsigned)L.shmem, st, args,
                                  nullptr));
@@ -1784,6 +1813,23 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     dense_keys *= (double)std::max<size_t>(m.size(), 1);
     r->keys.push_back(std::move(m));
   }
+  // Matching docs per segment, counted once at plan time by a filter-only pass when a planning decision
+  // needs them (numGroupsLimit trimming, the selection-vector plan); segments are immutable, so the
+  // counts hold for every re-execution of the plan.
+  std::vector<int64_t> seg_matched;
+  auto probe_matched = [&]() -> int {
+    if (!seg_matched.empty()) return 0;
+    pinot_amd_query fq;
+    fq.preds = Q.preds;
+    pinot_amd_result* fr = nullptr;
+    if (int rc = execute_impl(&fq, segs.data(), n, stream, true, &fr)) return rc;
+    std::unique_ptr<pinot_amd_result> hold(fr);
+    seg_matched.assign(n, 0);
+    for (int si = 0; si < n; ++si)
+      if (int rc = pinot_amd_bitset_count((const uint64_t*)fr->bitsets[si]->p, segs[si]->num_docs, &seg_matched[si], stream))
+        return rc;
+    return 0;
+  };
   // numGroupsLimit: a segment can only reach the limit if it can hold that many keys (matching docs
   // and its own dictionaries' key space bound it); otherwise no trimming can happen
   std::vector<int64_t> seg_bound(n, 0);
@@ -1801,16 +1847,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     // docs too (a segment's groups <= its matching docs). Counted once at plan time by a filter-only
     // pass; segments are immutable, so the counts hold for every re-execution of the plan.
     if (limit_possible && !Q.preds.empty() && !env_is("PINOT_AMD_TRIM_PROBE", "0")) {
-      pinot_amd_query fq;
-      fq.preds = Q.preds;
-      pinot_amd_result* fr = nullptr;
-      if (int rc = execute_impl(&fq, segs.data(), n, stream, true, &fr)) return rc;
-      std::unique_ptr<pinot_amd_result> hold(fr);
+      if (int rc = probe_matched()) return rc;
       limit_possible = false;
       for (int si = 0; si < n; ++si) {
-        int64_t cnt = 0;
-        if (int rc = pinot_amd_bitset_count((const uint64_t*)fr->bitsets[si]->p, segs[si]->num_docs, &cnt, stream)) return rc;
-        seg_bound[si] = std::min(seg_bound[si], cnt);
+        seg_bound[si] = std::min(seg_bound[si], seg_matched[si]);
         limit_possible |= seg_bound[si] >= Q.num_groups_limit;
       }
     }
@@ -2145,6 +2185,68 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (size_t j = 0; j < Q.group_by.size(); ++j) base.hash_pack.push_back({r->pack_word[j], r->pack_shift[j]});
   }
 
+  // ---- selection-vector plan (late materialisation) ----
+  // A selective filter over narrow rows: the select pass reads only the filter columns and appends the
+  // matching docIds; the gather pass reads the group-by / aggregated columns of those docs only (64 B
+  // sectors at random positions). Chosen when its bytes, from the exact per-segment match counts,
+  // undercut the fused scan's: filter columns + 16 B per match (vector write + read) + the value columns'
+  // sectors a match touches + a per-match gather cost, against every column of every doc.
+  std::vector<bool> leaf_slot(nslots, false), value_slot(nslots, false);
+  for (size_t pi = 0; pi < np; ++pi)
+    if (pred_slot[pi] >= 0) leaf_slot[pred_slot[pi]] = true;
+  for (auto& g : base.group) value_slot[g.first] = true;
+  for (auto& a : base.accs)
+    if (a.op != ACC_FIRST_DOC) {
+      value_slot[a.slot] = true;
+      if (a.expr != EXPR_COL) value_slot[a.slot2] = true;
+    }
+  auto slot_bpr = [](const DevColumn& c) -> double {
+    return c.enc == ENC_FIXED_BIT ? c.bits / 8.0 : c.enc == ENC_RAW ? (double)value_size(c.type) : 0.0;
+  };
+  const char* sel_env = getenv("PINOT_AMD_SELECT");
+  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !base.partitioned &&
+                            (r->kind == PLAN_DENSE || r->kind == PLAN_HASH) && !(sel_env && !strcmp(sel_env, "never"));
+  if (sel_eligible) {
+    double scan_b = 0, leaf_b = 0;
+    for (int si = 0; si < n; ++si)
+      for (int sl = 0; sl < nslots; ++sl) {
+        const double b = slot_bpr(hsegs[si].cols[sl]) * (double)segs[si]->num_docs;
+        scan_b += b;
+        if (leaf_slot[sl]) leaf_b += b;
+      }
+    const bool forced = sel_env && !strcmp(sel_env, "always");
+    if (forced || leaf_b < 0.75 * scan_b) {  // the select pass alone could win: count the matches
+      if (int rc = probe_matched()) return rc;
+      double sel_b = leaf_b;
+      for (int si = 0; si < n; ++si) {
+        const double m = (double)seg_matched[si], docs = (double)std::max<int64_t>(segs[si]->num_docs, 1);
+        const double s = m / docs;
+        sel_b += 24.0 * m;  // vector write + read, and the per-doc gather work
+        for (int sl = 0; sl < nslots; ++sl) {
+          if (!value_slot[sl]) continue;
+          const DevColumn& c = hsegs[si].cols[sl];
+          const double bpr = slot_bpr(c);
+          if (bpr <= 0) continue;
+          const double per_sector = 64.0 / bpr;  // docs per 64-byte sector
+          sel_b += bpr * docs * (1.0 - std::pow(1.0 - s, per_sector));
+        }
+      }
+      base.select = forced || sel_b < 0.75 * scan_b;
+    }
+    if (base.select && base.lds) {
+      // gather blocks may add up to ceil(matches / CUs) + 4 x block docs to one LDS table: re-bound the
+      // narrow 64-bit partials for that and keep the table within the LDS
+      const int64_t scan_min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
+      const __int128 scan_bound = (__int128)((all_tiles + scan_min_grid - 1) / scan_min_grid) * kTileDocs;
+      const __int128 gather_bound = (__int128)((all_docs + cus - 1) / cus) + 4 * 256 * base.scan_nsub;
+      if (gather_bound > scan_bound) {
+        set_narrow(gather_bound);
+        lds_bytes = lds_arrays() * std::max<int64_t>(num_keys, 1) * 8;
+        if (lds_bytes > lds_max) base.select = false;
+      }
+    }
+  }
+
   // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
   const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
   std::vector<int32_t> key_seg(n, 0);
@@ -2196,6 +2298,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   if (int rc = r->matched.alloc((3 * nl + 2) * sizeof(unsigned long long))) return rc;
   HIP_OK(hipMemset(r->matched.p, 0, r->matched.n));
   size_t max_count_cells = 0, max_rec = 0;
+  int64_t max_sel = 0;  // selection-vector entries of the largest select launch
   for (size_t li = 0; li < nl; ++li) {
     Launch& L = r->launches[li];
     std::vector<DevSegment> ls;
@@ -2279,6 +2382,11 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         if (jl.kinds != (1u << LEAF_DOC_BITSET) || jl.negate) gate[jl.clause] = 0;
       }
       for (int c = 0; c < nclauses; ++c) L.gated |= gate[c] && has[c];
+      // gated plans: column loads D tiles ahead of their gate, gate words 2D ahead. Measured on the
+      // inverted-index sweep, deeper pipelines only add registers (the gated loop is bound by its
+      // per-tile overhead, not by load latency), so the row-width depth stays unless overridden.
+      if (L.gated && getenv("PINOT_AMD_GATE_DEPTH"))
+        jp.depth = (int)std::min<int64_t>(std::max<int64_t>(env_i64("PINOT_AMD_GATE_DEPTH", 1), 1), 4);
     }
     L.jit = jit_get(jp, &r->jit_status);
     if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
@@ -2340,6 +2448,29 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
       }
       L.part.counts = (unsigned long long*)r->matched.p + 3 * li;
+    } else if (jp.select) {
+      // select pass: plain 256-thread blocks without LDS; gather pass: the table's block size and LDS
+      L.select = true;
+      L.scan_nsub = 1;
+      L.gather_threads = jp.lds ? kBlock * jp.scan_nsub : kBlock;
+      int nb = 0, ng = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
+          ng < 1)
+        ng = 1;
+      per_cu = nb;
+      L.gather_grid = cus * ng;
+      for (size_t k = 0; k < L.segs.size(); ++k)
+        for (int sl = 0; sl < nslots; ++sl) {
+          const double bpr = slot_bpr(ls[k].cols[sl]);
+          if (leaf_slot[sl]) L.filter_bytes += bpr * (double)ls[k].num_docs;
+          if (value_slot[sl] && k == 0) L.value_bpr += bpr;
+        }
+      // exact capacity: the launch's matching docs (plan-time counts) + at most 3 padding entries per
+      // wave run (one run per 256-doc wave tile)
+      int64_t m = 0;
+      for (int si : L.segs) m += seg_matched[si] + 3 * ((segs[si]->num_docs + 255) / 256 + 1);
+      max_sel = std::max<int64_t>(max_sel, m + 64);
     } else {
       int nb = 0;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||
@@ -2367,6 +2498,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.part.offs = (int64_t*)r->offs.p;
       L.part.part_begin = (int64_t*)r->part_begin.p;
       L.part.rec = (uint8_t*)r->rec.p;
+    }
+  }
+  // selection vector + per-launch counters (entries appended, runs that did not fit)
+  if (max_sel > 0) {
+    if (int rc = r->sel.alloc((size_t)max_sel * 8)) return rc;
+    if (int rc = r->sel_ctr.alloc(r->launches.size() * 16)) return rc;
+    for (size_t li = 0; li < r->launches.size(); ++li) {
+      Launch& L = r->launches[li];
+      L.q.sel_entries = (unsigned long long*)r->sel.p;
+      L.q.sel_count = (unsigned long long*)r->sel_ctr.p + 2 * li;
+      L.q.sel_cap = max_sel;
     }
   }
   // accumulator tables
@@ -2487,7 +2629,10 @@ int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes) {
   for (const auto& il : r->inv_leaves) b += il.alg_bytes;
   for (size_t li = 0; li < r->launches.size(); ++li) {
     const Launch& L = r->launches[li];
-    if (!L.gated || L.docs == 0) {
+    if (L.select) {  // filter columns of every doc, the vector written and read, the gathered columns
+      const double m = (double)c[3 * li];
+      b += L.filter_bytes + m * (16.0 + L.value_bpr);
+    } else if (!L.gated || L.docs == 0) {
       b += L.col_bytes;
     } else {  // gated: only the rows that pass the filter need their column bytes
       const double m = (double)std::max(c[3 * li], c[3 * li + 2]);
@@ -2506,6 +2651,11 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
     case PLAN_HASH: info = r->trim ? "jit-hash-trim" : "jit-hash"; break;
     default: info = "jit";
   }
+  for (const auto& L : r->launches)
+    if (L.select) {
+      info += "-select";
+      break;
+    }
   if (r->launches.size() > 1) info += " x" + std::to_string(r->launches.size());
   return info.c_str();
 }
@@ -2530,6 +2680,14 @@ static int compact_groups(pinot_amd_result* r) {
   if (c[3 * r->launches.size() + 1] != 0)
     return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
                 (long long)c[3 * r->launches.size() + 1]);
+  if (r->sel_ctr.n) {
+    std::vector<unsigned long long> sc(r->sel_ctr.n / 8);
+    HIP_OK(hipMemcpyAsync(sc.data(), r->sel_ctr.p, r->sel_ctr.n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (size_t li = 0; li < sc.size() / 2; ++li)
+      if (sc[2 * li + 1] != 0)
+        return fail(PINOT_AMD_EOVERFLOW, "selection vector of launch %zu overflowed (%llu runs dropped)", li, sc[2 * li + 1]);
+  }
   if (r->num_group_by == 0 || r->q.nacc == 0) {
     r->ngroups = 1;
     r->ckeys.assign(1, 0);

@@ -80,6 +80,9 @@ struct JitPlan {
   int hash_words = 0;          // key words including the segment word
   bool hash_seg = false;
   std::vector<std::pair<int, int>> hash_pack;
+  // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
+  // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
+  bool select = false;
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals)
 void jit_layout_records(JitPlan* p);
@@ -94,6 +97,7 @@ struct JitKernel {
   hipFunction_t fn = nullptr;          // pinot_scan_jit, or the partition count pass
   hipFunction_t fn_scatter = nullptr;  // partitioned: scatter pass
   hipFunction_t fn_agg = nullptr;      // partitioned: LDS aggregation of the partitions
+  hipFunction_t fn_gather = nullptr;   // selection-vector plans: the gather-aggregate pass (fn = select)
 };
 // C type / size of an accumulated value: a column's decoded value type; an expression is int64
 // when both operands are INT (exact), else double (the transforms' DOUBLE result)
