@@ -89,6 +89,7 @@ struct DevPartition {
   int64_t* offs;
   int64_t* part_begin;
   uint8_t* rec;
+  int64_t vbase[kMaxAcc];    // packed records: integer value j is stored as value - vbase[j]
 };
 
 // Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the

@@ -2147,6 +2147,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     return (int64_t)k;
   };
   int64_t lds_bytes = (int64_t)q.nacc * std::max<int64_t>(num_keys, 1) * 8;
+  std::vector<int64_t> part_vbase;  // partitioned plans: integer record fields' bases (DevPartition::vbase)
   if (r->kind == PLAN_DENSE && q.nacc > 0) {
     const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
     set_narrow((__int128)((all_tiles + min_grid - 1) / min_grid) * kTileDocs);
@@ -2173,6 +2174,62 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (a.op != ACC_HI && a.op != ACC_FIRST_DOC &&
               std::find(base.vals.begin(), base.vals.end(), a.val()) == base.vals.end())
             base.vals.push_back(a.val());
+        // packed record fields: an integer value is stored as value - lo in bitlen(hi - lo) bits, where
+        // [lo, hi] is the batch's value range (dictionary ends / staged min-max; interval arithmetic for
+        // times / minus / plus of two INT columns); without a range INT takes 32 bits above INT32_MIN,
+        // LONG 64. FLOAT / DOUBLE values keep their raw bits.
+        auto slot_range = [&](int sl, __int128* lo, __int128* hi) {
+          bool any = false;
+          for (auto* s : segs) {
+            const Column& c = *s->cols.at(slot_cols[sl]);
+            if (s->num_docs == 0) continue;
+            if (!c.has_range) return false;
+            if (!any || c.vmin < *lo) *lo = c.vmin;
+            if (!any || c.vmax > *hi) *hi = c.vmax;
+            any = true;
+          }
+          if (!any) *lo = *hi = 0;
+          return true;
+        };
+        base.val_bits.clear();
+        part_vbase.clear();
+        for (const JitVal& v : base.vals) {
+          auto slot_type = [&](int sl) { return segs[0]->cols.at(slot_cols[sl])->type; };
+          const int t1 = slot_type(v.slot), t2 = v.expr == EXPR_COL ? T_INT : slot_type(v.slot2);
+          const bool is_int = v.expr == EXPR_COL ? (t1 == T_INT || t1 == T_LONG) : (t1 == T_INT && t2 == T_INT);
+          if (!is_int) {
+            base.val_bits.push_back(v.expr == EXPR_COL && t1 == T_FLOAT ? 32 : 64);
+            part_vbase.push_back(0);
+            continue;
+          }
+          __int128 lo = 0, hi = 0, lo2 = 0, hi2 = 0;
+          bool known = slot_range(v.slot, &lo, &hi);
+          if (known && v.expr != EXPR_COL) {
+            known = slot_range(v.slot2, &lo2, &hi2);
+            if (v.expr == EXPR_ADD) {
+              lo += lo2;
+              hi += hi2;
+            } else if (v.expr == EXPR_SUB) {
+              const __int128 l = lo - hi2, h = hi - lo2;
+              lo = l;
+              hi = h;
+            } else {
+              const __int128 c[4] = {lo * lo2, lo * hi2, hi * lo2, hi * hi2};
+              lo = *std::min_element(c, c + 4);
+              hi = *std::max_element(c, c + 4);
+            }
+          }
+          if (!known) {
+            const bool narrow = v.expr == EXPR_COL && t1 == T_INT;
+            base.val_bits.push_back(narrow ? 32 : 64);
+            part_vbase.push_back(narrow ? INT32_MIN : 0);
+            continue;
+          }
+          int bits = 0;
+          for (unsigned __int128 w = (unsigned __int128)(hi - lo); w; w >>= 1) ++bits;
+          base.val_bits.push_back(std::min(bits, 64));
+          part_vbase.push_back((int64_t)lo);
+        }
       }
     }
   }
@@ -2423,6 +2480,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       L.part.nparts = jp.nparts;
       L.part.key_shift = jp.key_shift;
+      for (size_t j = 0; j < part_vbase.size() && j < (size_t)kMaxAcc; ++j) L.part.vbase[j] = part_vbase[j];
       L.shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
       L.shmem_agg = (size_t)lds_arrays() * ((size_t)1 << jp.key_shift) * 8;
       L.shmem = (size_t)jp.nparts * 4;

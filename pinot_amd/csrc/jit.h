@@ -71,8 +71,13 @@ struct JitPlan {
   int key_shift = 0;           // keys per partition = 2^key_shift
   int nparts = 0;
   std::vector<JitVal> vals;    // record values (distinct values read by accumulators)
-  std::vector<int> val_off;    // byte offset of each value column in a record (key u32 at 0)
-  int rec_bytes = 0;           // record size, multiple of 8
+  // Bit-packed records: the partition-local key in bits [0, key_shift), then value j's field of
+  // val_bits[j] bits at bit val_off[j]. An integer field holds value - DevPartition::vbase[j] (the
+  // batch's value range bounds it; val_bits 0: the value is constant), a FLOAT / DOUBLE field the raw
+  // bits. Filled by jit_layout_records; val_bits may be preset by the planner (empty: natural widths).
+  std::vector<int> val_bits;
+  std::vector<int> val_off;
+  int rec_bytes = 0;           // record size: 64-bit words x 8
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
   // hash-table GROUP BY (DevHash): group column j's merged id goes to key word hash_pack[j].first at
   // bit hash_pack[j].second; hash_seg appends the segment's key_seg as the last word (trimming)
@@ -84,8 +89,12 @@ struct JitPlan {
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;
 };
-// record layout of a partitioned plan (fills val_off / rec_bytes from vals)
+// record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);
+// natural field width of a record value (no range known): 32 for INT / FLOAT, else 64
+int jit_val_natural_bits(const JitPlan& p, const JitVal& v);
+// whether record value v is stored as an integer offset from its base (else as raw float bits)
+bool jit_val_is_int(const JitPlan& p, const JitVal& v);
 // LDS bytes of the scatter pass for a staging capacity
 size_t jit_scatter_lds(const JitPlan& p, int cap);
 // LDS-privatised table layout: accumulator -> LDS array (-1: the high word of a narrow 128-bit sum,

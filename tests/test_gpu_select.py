@@ -46,7 +46,7 @@ QUERIES = [
     # inverted-index leaf + raw IN, group by the sorted column
     "SELECT ts, COUNT(*), SUM(r_double), MIN(r_long) FROM t WHERE d1 IN (10, 17, 73) OR r_int IN (5, 77, 1000) GROUP BY ts",
     # CU-wide LDS table (37 x 300 keys) and an expression
-    "SELECT d1, fd, COUNT(*), SUM(times(r_int, d1)), MAX(r_long) FROM t WHERE d2 < 700 GROUP BY d1, fd",
+    "SELECT d1, fd, COUNT(*), SUM(r_int * d1), MAX(r_long) FROM t WHERE d2 < 700 GROUP BY d1, fd",
     # HBM table (3000 x 37 keys)
     "SELECT d0, d1, COUNT(*), SUM(r_long), MIN(r_int) FROM t WHERE d2 BETWEEN 100 AND 600 AND r_double > 0 GROUP BY d0, d1",
     # nothing matches / everything matches
@@ -61,6 +61,8 @@ def test_forced_select_vs_oracle(engine, data, monkeypatch, qi, plan):
     monkeypatch.setenv("PINOT_AMD_SELECT", "always")
     if plan == "hash":
         monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    else:  # the HBM-table query's 111k keys would otherwise take the partitioned plan
+        monkeypatch.setenv("PINOT_AMD_PARTITIONED", "0")
     bufs, segs = data
     q = QUERIES[qi]
     res = engine.ServerQueryExecutor().execute(q, segs)
