@@ -76,10 +76,15 @@ struct DevSegment {
 //   scan:         offs[p * grid + block] = exclusive prefix within partition p; part_begin = prefix
 //                 of partition totals (part_begin[nparts] = all records)
 //   scatter pass: record r of partition p at part_begin[p] + offs[..] + running index, staged per
-//                 partition in LDS and written out in runs; a record is `rec_bytes` bytes at
-//                 rec + r * rec_bytes: u32 local key (key & (2^key_shift - 1)), then the values of
-//                 the accumulated columns (4-byte values first, then 8-byte values, 8-B aligned)
+//                 partition in LDS and written out in runs; a record is `rec_bytes` bytes (whole
+//                 64-bit words) at rec + r * rec_bytes, bit-packed: the local key (key & (2^key_shift
+//                 - 1)) in the low bits, then one field per accumulated value (JitPlan::val_bits /
+//                 val_off; integers as value - vbase[j], FLOAT / DOUBLE as raw bits)
 //   agg pass:     one LDS table of 2^key_shift keys per partition, flushed with global atomics
+// Sampled plans (JitPlan::part_sampled) replace the count pass with a histogram over every
+// sample_stride-th tile of each scatter block's range: block b gets an allotment of records of
+// partition p sized from its own sample (with a margin for the sampling error); what does not fit
+// goes to the overflow slab (ovf_rec / ovf_part), which pinot_part_ovf adds into the HBM table directly.
 struct DevPartition {
   int32_t nparts, key_shift;
   int64_t atomic_threshold;  // records <= this: the direct-atomic scan runs instead of scatter + agg
@@ -90,6 +95,14 @@ struct DevPartition {
   int64_t* part_begin;
   uint8_t* rec;
   int64_t vbase[kMaxAcc];    // packed records: integer value j is stored as value - vbase[j]
+  // sampled plans (JitPlan::part_sampled): offs[c] = first record of allotment c = p * seg_grid + b
+  // (partition p, scatter block b; offs[c + 1] ends it); after the scatter hist[c] = the records it
+  // holds and eff_begin = their exclusive prefix, the aggregation pass's record index space
+  int64_t seg_grid;
+  int64_t* eff_begin;
+  uint8_t* ovf_rec;          // overflow slab: records, their partitions, and the count
+  uint32_t* ovf_part;
+  unsigned long long* ovf_n;
 };
 
 // Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the

@@ -57,6 +57,8 @@ hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const i
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
 hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
                                     int64_t* d_part_begin, hipStream_t st);
+hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int mode, int64_t stride, double scale,
+                               int64_t limit, int64_t* d_ptot, int64_t* d_out, hipStream_t st);
 }  // namespace pamd
 
 using namespace pamd;
@@ -1060,6 +1062,10 @@ struct Launch {
   bool select = false;
   int gather_grid = 1, gather_threads = 256;
   double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
+  // partitioned: record size; sampled capacities (strided histogram instead of the count pass)
+  int rec_bytes = 0;
+  bool part_sampled = false;
+  int64_t region_cap = 0;  // records the partition regions can hold
 };
 
 enum PlanKind { PLAN_DENSE = 0, PLAN_PARTITIONED = 1, PLAN_HASH = 2, PLAN_FILTER = 3 };
@@ -1100,6 +1106,7 @@ struct pinot_amd_result {
   std::string jit_status;
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
+  DevBuf eff_begin, ovf_n, ovf_rec, ovf_part;  // sampled plans: allotment prefix, overflow slab
   // selection-vector plans: the shared vector (launches run one after another) and 2 counters per launch
   DevBuf sel, sel_ctr;
   // hash-table GROUP BY
@@ -1585,6 +1592,30 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   }
   const unsigned pt = (unsigned)(kBlock * kPartSub);
   const unsigned count_grid = (unsigned)(L.grid * kPartCountRatio);
+  if (L.part_sampled) {
+    // per scatter block: strided histogram -> allotments -> (direct-atomic scan | scatter) -> records
+    // held per allotment -> aggregation -> overflow slab
+    unsigned long long* sampled = matched + 1;
+    void* sargs[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&sampled, (void*)&L.part, (void*)&h};
+    HIP_OK(hipMemsetAsync(L.part.ovf_n, 0, 8, st));
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem, st, sargs, nullptr));
+    static const double cap_scale = []() {
+      const char* v = getenv("PINOT_AMD_PART_CAP_SCALE");  // tests: < 1 forces records into the slab
+      return v ? std::max(0.0, atof(v)) : 1.0;
+    }();
+    HIP_OK(launch_allot_prefix(L.part.hist, L.part.nparts, L.grid, 0, L.part.sample_stride, cap_scale, L.region_cap,
+                               L.part.part_begin, L.part.offs, st));
+    if (L.jit_atomic)
+      HIP_OK(hipModuleLaunchKernel(L.jit_atomic->fn, (unsigned)L.atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn_scatter, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem_scatter, st, args,
+                                 nullptr));
+    HIP_OK(launch_allot_prefix(L.part.hist, L.part.nparts, L.grid, 1, 1, 1.0, 0, L.part.part_begin, L.part.eff_begin, st));
+    void* agg_args[] = {(void*)&L.part, (void*)&table};
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn_agg, (unsigned)L.agg_grid, 1, 1, 1024, 1, 1, (unsigned)L.shmem_agg, st,
+                                 agg_args, nullptr));
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn_ovf, (unsigned)(4 * L.agg_grid), 1, 1, 256, 1, 1, 0, st, agg_args, nullptr));
+    return 0;
+  }
   if (L.jit_sample) {
     unsigned long long* sampled = matched + 1;
     void* sargs[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&sampled, (void*)&L.part, (void*)&h};
@@ -2162,10 +2193,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // each partition in LDS (random per-lane HBM atomics run ~17x below the coalesced rate)
       set_narrow((__int128)((all_docs + cus - 1) / cus));
       const int64_t na = lds_arrays();
+      // the aggregation block's LDS: the partition's table + (sampled plans) its allotment tables,
+      // 2 x 8 B per scatter block (<= 2 x CUs blocks)
+      const int64_t agg_lds = lds_max - (2 * 2 * (int64_t)cus + 1) * 8;
       int shift = 16;
-      while (shift > 6 && na * ((int64_t)1 << shift) * 8 > lds_max) --shift;
+      while (shift > 6 && na * ((int64_t)1 << shift) * 8 > agg_lds) --shift;
       const int64_t nparts = (num_keys + ((int64_t)1 << shift) - 1) >> shift;
-      if (na * ((int64_t)1 << shift) * 8 <= lds_max && nparts <= 8192) {
+      if (na * ((int64_t)1 << shift) * 8 <= agg_lds && nparts <= 8192) {
         r->kind = PLAN_PARTITIONED;
         base.partitioned = true;
         base.key_shift = shift;
@@ -2354,7 +2388,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const size_t nl = r->launches.size();
   if (int rc = r->matched.alloc((3 * nl + 2) * sizeof(unsigned long long))) return rc;
   HIP_OK(hipMemset(r->matched.p, 0, r->matched.n));
-  size_t max_count_cells = 0, max_rec = 0;
+  size_t max_count_cells = 0, max_rec = 0, max_slab = 0, max_slab_docs = 0;
   int64_t max_sel = 0;  // selection-vector entries of the largest select launch
   for (size_t li = 0; li < nl; ++li) {
     Launch& L = r->launches[li];
@@ -2419,6 +2453,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);
+      // sampled allotments replace the exact count pass once the strided histogram has >= 64 tiles
+      const int64_t stride = env_i64("PINOT_AMD_SAMPLE_STRIDE", 32);
+      jp.part_sampled = stride > 0 && tiles >= 64 * stride && !env_is("PINOT_AMD_PART_SAMPLED", "0");
+      if (jp.part_sampled) L.part.sample_stride = stride;
       // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a run is
       // too short to pay for the staging round trip and records are written directly
       int cap = 64;
@@ -2469,7 +2507,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // selectivity sample over every 32nd tile: when the extrapolated matches fall under the threshold
       // the count pass steps aside and the direct-atomic scan is the only full pass
       const int64_t stride = env_i64("PINOT_AMD_SAMPLE_STRIDE", 32);
-      if (L.jit_atomic && stride > 0 && tiles >= 64 * stride) {
+      if (!jp.part_sampled && L.jit_atomic && stride > 0 && tiles >= 64 * stride) {
         JitPlan js = ja;
         js.atomic_gate = false;
         js.sample = true;
@@ -2484,7 +2522,16 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.shmem_scatter = jit_scatter_lds(jp, jp.stage_cap);
       L.shmem_agg = (size_t)lds_arrays() * ((size_t)1 << jp.key_shift) * 8;
       L.shmem = (size_t)jp.nparts * 4;
-      max_rec = std::max(max_rec, (size_t)L.docs * jp.rec_bytes + 256);
+      L.rec_bytes = jp.rec_bytes;
+      L.part_sampled = jp.part_sampled;
+      // sampled plans: the allotments may take 1.5 x docs + 256 records per partition (scaled to fit),
+      // the overflow slab every doc (it can never fill up)
+      L.region_cap = L.docs + L.docs / 2 + 256 * (int64_t)jp.nparts;
+      max_rec = std::max(max_rec, (size_t)(jp.part_sampled ? L.region_cap : L.docs) * jp.rec_bytes + 256);
+      if (jp.part_sampled) {
+        max_slab = std::max(max_slab, (size_t)L.docs * jp.rec_bytes + 256);
+        max_slab_docs = std::max(max_slab_docs, (size_t)L.docs + 64);
+      }
       int nb = 0;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn_scatter, kBlock * kPartSub, L.shmem_scatter) !=
               hipSuccess || nb < 1)
@@ -2540,6 +2587,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
     if ((jp.partitioned || L.scan_nsub > 1) && grid * kPartSub > tiles) grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
+    if (L.part_sampled) {  // allotment tables of <= 2 x CUs scatter blocks sit behind the aggregation table
+      grid = std::min<int64_t>(grid, 2 * (int64_t)cus);
+      L.shmem_agg += (size_t)(2 * grid + 1) * 8;
+    }
     L.grid = (int)grid;
     if (jp.partitioned) max_count_cells = std::max(max_count_cells, (size_t)jp.nparts * (size_t)grid * kPartCountRatio);
   }
@@ -2551,11 +2602,24 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (int rc = r->offs.alloc(max_count_cells * 8)) return rc;
     if (int rc = r->part_begin.alloc(((size_t)maxp + 1) * 8)) return rc;
     if (int rc = r->rec.alloc(max_rec)) return rc;
+    if (max_slab > 0) {
+      if (int rc = r->eff_begin.alloc(max_count_cells * 8 + 8)) return rc;
+      if (int rc = r->ovf_n.alloc(8)) return rc;
+      if (int rc = r->ovf_rec.alloc(max_slab)) return rc;
+      if (int rc = r->ovf_part.alloc(max_slab_docs * 4)) return rc;
+    }
     for (auto& L : r->launches) {
       L.part.hist = (uint32_t*)r->hist.p;
       L.part.offs = (int64_t*)r->offs.p;
       L.part.part_begin = (int64_t*)r->part_begin.p;
       L.part.rec = (uint8_t*)r->rec.p;
+      if (L.part_sampled) {
+        L.part.seg_grid = L.grid;
+        L.part.ovf_n = (unsigned long long*)r->ovf_n.p;
+        L.part.eff_begin = (int64_t*)r->eff_begin.p;
+        L.part.ovf_rec = (uint8_t*)r->ovf_rec.p;
+        L.part.ovf_part = (uint32_t*)r->ovf_part.p;
+      }
     }
   }
   // selection vector + per-launch counters (entries appended, runs that did not fit)

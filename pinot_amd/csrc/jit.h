@@ -79,6 +79,12 @@ struct JitPlan {
   std::vector<int> val_off;
   int rec_bytes = 0;           // record size: 64-bit words x 8
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
+  // Sampled capacities instead of the exact count pass: a histogram over every sample_stride-th tile
+  // sizes each partition's region (DevPartition::cap); the scatter reserves space with one global
+  // atomic per flushed run, records beyond a region's capacity go to the overflow slab, aggregated
+  // by pinot_part_ovf with direct HBM atomics. The paired direct-atomic scan (atomic_gate) then also
+  // decides from the sample.
+  bool part_sampled = false;
   // hash-table GROUP BY (DevHash): group column j's merged id goes to key word hash_pack[j].first at
   // bit hash_pack[j].second; hash_seg appends the segment's key_seg as the last word (trimming)
   bool hash = false;
@@ -106,6 +112,7 @@ struct JitKernel {
   hipFunction_t fn = nullptr;          // pinot_scan_jit, or the partition count pass
   hipFunction_t fn_scatter = nullptr;  // partitioned: scatter pass
   hipFunction_t fn_agg = nullptr;      // partitioned: LDS aggregation of the partitions
+  hipFunction_t fn_ovf = nullptr;      // sampled partitioned: the overflow slab's direct atomics
   hipFunction_t fn_gather = nullptr;   // selection-vector plans: the gather-aggregate pass (fn = select)
 };
 // C type / size of an accumulated value: a column's decoded value type; an expression is int64

@@ -395,6 +395,82 @@ __global__ void exclusive_scan_kernel(int64_t* counts, int64_t n, int64_t* total
   if (threadIdx.x == 0) *total = carry;
 }
 
+// Sampled partitioned plans (JitPlan::part_sampled), allotment c = p * G + b (partition p, scatter
+// block b). Two launches of P blocks turn per-allotment sizes into their exclusive prefix (P * G + 1
+// entries): the first writes each partition's local prefix over b and its total, the second adds the
+// partition's base (sum of the totals before it) and, if the whole exceeds `limit`, scales the prefix
+// down to fit (floor of a monotone prefix stays monotone, so every size stays >= 0).
+//   mode 0 (allotments): size = (e + e/16 + 3 x stride x (sqrt(s) + 1)) x scale from the strided
+//          histogram hist[c] = s (e = stride x s: a 3-sigma margin on the sampling error);
+//   mode 1 (after the scatter): size = hist[c], the records allotment c holds.
+__device__ __forceinline__ int64_t allot_size(const uint32_t* hist, int64_t c, int mode, int64_t stride, double scale) {
+  const double sm = (double)hist[c];
+  if (mode) return (int64_t)hist[c];
+  const double e = sm * (double)stride;
+  return (int64_t)min((e + e / 16.0 + 3.0 * (double)stride * (sqrt(sm) + 1.0)) * scale, 4.0e9);
+}
+
+__global__ void __launch_bounds__(256) allot_local_kernel(const uint32_t* hist, int64_t G, int mode, int64_t stride,
+                                                         double scale, int64_t* out, int64_t* ptot) {
+  __shared__ int64_t carry;
+  __shared__ int64_t wsum[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t p = blockIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < G; b0 += 256) {
+    const int64_t b = b0 + t;
+    const int64_t x = b < G ? allot_size(hist, p * G + b, mode, stride, scale) : 0;
+    int64_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    if (b < G) out[p * G + b] = before + incl - x;
+    __syncthreads();
+    if (t == 255) carry = before + incl;
+    __syncthreads();
+  }
+  if (t == 0) ptot[p] = carry;
+}
+
+__global__ void __launch_bounds__(256) allot_base_kernel(const int64_t* ptot, int32_t P, int64_t G, int64_t limit,
+                                                        int64_t* out) {
+  __shared__ int64_t red[256];
+  const int t = threadIdx.x;
+  const int64_t p = blockIdx.x;
+  int64_t base = 0, all = 0;
+  for (int64_t q = t; q < P; q += 256) {
+    all += ptot[q];
+    if (q < p) base += ptot[q];
+  }
+  red[t] = base;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  base = red[0];
+  __syncthreads();
+  red[t] = all;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  all = red[0];
+  const double f = (limit > 0 && all > limit) ? (double)limit / (double)all : 1.0;
+  for (int64_t b = t; b < G; b += 256) {
+    const int64_t v = base + out[p * G + b];
+    out[p * G + b] = f < 1.0 ? (int64_t)((double)v * f) : v;
+  }
+  if (p == P - 1 && t == 0) out[(int64_t)P * G] = f < 1.0 ? (int64_t)((double)all * f) : all;
+}
+
 // Partitioned GROUP BY offsets (DevPartition): row p of hist holds the per-block record counts of
 // partition p; one block per row turns it into exclusive per-block offsets and the row total.
 __global__ void partition_row_scan_kernel(const uint32_t* hist, int64_t nblocks, int64_t* offs, int64_t* row_total) {
@@ -924,6 +1000,14 @@ hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int6
                      d_part_begin);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, d_part_begin, (int64_t)nparts,
                      d_part_begin + nparts);
+  return hipGetLastError();
+}
+
+hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int mode, int64_t stride, double scale,
+                               int64_t limit, int64_t* d_ptot, int64_t* d_out, hipStream_t st) {
+  if (P <= 0) return hipSuccess;
+  hipLaunchKernelGGL(allot_local_kernel, dim3((unsigned)P), dim3(256), 0, st, d_hist, G, mode, stride, scale, d_out, d_ptot);
+  hipLaunchKernelGGL(allot_base_kernel, dim3((unsigned)P), dim3(256), 0, st, d_ptot, P, G, limit, d_out);
   return hipGetLastError();
 }
 

@@ -76,3 +76,38 @@ def test_packed_records_vs_oracle(engine, monkeypatch, qi):
     assert_same_groups(res.groups(), og, fs)
     res.execute_again()
     assert_same_groups(res.groups(), og, fs)
+
+
+@pytest.mark.parametrize("scale,stage_cap,where", [
+    (None, None, ""),                  # sampled capacities as planned (stride 1: the sample is exact)
+    ("0.5", None, ""),                 # half the needed capacity: the rest goes to the overflow slab
+    ("0", None, ""),                   # no capacity at all: every record through the slab
+    ("0.7", "0", ""),                  # direct writes (no LDS staging), reservations per record
+    (None, None, " WHERE x < -29500"),  # ~0.8 % match: the sample hands over to the direct-atomic scan
+])
+def test_sampled_capacities_vs_oracle(engine, monkeypatch, scale, stage_cap, where):
+    """Sampled partitioned plans (strided histogram instead of the exact count pass; reservations per
+    flushed run; records beyond a partition's capacity through the overflow slab's direct atomics):
+    identical groups to the oracle whatever the capacities."""
+    monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
+    monkeypatch.delenv("PINOT_AMD_ATOMIC_HANDOVER", raising=False)
+    monkeypatch.setenv("PINOT_AMD_SAMPLE_STRIDE", "1")
+    for var, val in (("PINOT_AMD_PART_CAP_SCALE", scale), ("PINOT_AMD_STAGE_CAP", stage_cap)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, val)
+    rng = np.random.default_rng(5)
+    bufs = [_segment(rng, n, f"sc{i}", shift=i * 10) for i, n in enumerate([150_001, 90_000])]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = ("SET numGroupsLimit = 2000000; SELECT a, b, COUNT(*), SUM(x), MIN(l_nano), MAX(dbl), SUM(dbl) FROM t"
+         + where + " GROUP BY a, b")
+    qc = parse_sql(q)
+    res = engine.ServerQueryExecutor().execute(qc, segs)
+    assert res.kernel_info().startswith("jit-partitioned"), res.kernel_info()
+    nm, og = oracle.execute(qc, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og, {4})
+    res.execute_again()  # cursors and the slab reset per execution
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og, {4})
