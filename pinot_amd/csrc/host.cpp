@@ -2298,31 +2298,56 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !base.partitioned &&
                             (r->kind == PLAN_DENSE || r->kind == PLAN_HASH) && !(sel_env && !strcmp(sel_env, "never"));
   if (sel_eligible) {
-    double scan_b = 0, leaf_b = 0;
-    for (int si = 0; si < n; ++si)
+    // Cost in time, not bytes: a pass over a tile costs per-doc work as well as bytes (measured on one
+    // MI355X: a fused scan of narrow SSB rows and the select pass alike take ~1-1.3 ps per doc however
+    // few bytes they read; a gathered doc ~30-50 ps on SSB, more for scattered raw columns), so the
+    // selection-vector plan only pays when the value columns it skips are wide and few docs match.
+    constexpr double kBw = 6.0e12;         // achievable HBM read rate, B/s
+    constexpr double kScanDoc = 1.3e-12;   // fused scan, per doc
+    constexpr double kGatedDoc = 1.25e-12; // inverted-index gated scan, per doc
+    constexpr double kSelectDoc = 1.0e-12; // select pass, per doc
+    constexpr double kGatherDoc = 60e-12;  // gather pass, per matching doc
+    double scan_b = 0, leaf_b = 0, docs_all = 0;
+    for (int si = 0; si < n; ++si) {
+      docs_all += (double)segs[si]->num_docs;
       for (int sl = 0; sl < nslots; ++sl) {
         const double b = slot_bpr(hsegs[si].cols[sl]) * (double)segs[si]->num_docs;
         scan_b += b;
         if (leaf_slot[sl]) leaf_b += b;
       }
+    }
+    bool gated = false;  // some clause is all inverted-index bitsets: the fused scan reads columns only where it passes
+    {
+      std::vector<int> gate(nclauses, 1), has(nclauses, 0);
+      for (size_t k = 0; k < order.size(); ++k) {
+        const int c = Q.preds[order[k]].clause;
+        has[c] = 1;
+        for (int si = 0; si < n; ++si)
+          if (hsegs[si].leaves[k].kind != LEAF_DOC_BITSET || hsegs[si].leaves[k].negate) gate[c] = 0;
+      }
+      for (int c = 0; c < nclauses; ++c) gated |= gate[c] && has[c];
+    }
+    const double scan_t = std::max(scan_b / kBw, docs_all * (gated ? kGatedDoc : kScanDoc));
     const bool forced = sel_env && !strcmp(sel_env, "always");
-    if (forced || leaf_b < 0.75 * scan_b) {  // the select pass alone could win: count the matches
+    if (forced || std::max(leaf_b / kBw, docs_all * kSelectDoc) < 0.9 * scan_t) {  // the select pass alone could win
       if (int rc = probe_matched()) return rc;
-      double sel_b = leaf_b;
+      double sel_bytes = leaf_b, matches = 0;
       for (int si = 0; si < n; ++si) {
         const double m = (double)seg_matched[si], docs = (double)std::max<int64_t>(segs[si]->num_docs, 1);
         const double s = m / docs;
-        sel_b += 24.0 * m;  // vector write + read, and the per-doc gather work
+        matches += m;
+        sel_bytes += 16.0 * m;  // vector written + read
         for (int sl = 0; sl < nslots; ++sl) {
           if (!value_slot[sl]) continue;
           const DevColumn& c = hsegs[si].cols[sl];
           const double bpr = slot_bpr(c);
           if (bpr <= 0) continue;
           const double per_sector = 64.0 / bpr;  // docs per 64-byte sector
-          sel_b += bpr * docs * (1.0 - std::pow(1.0 - s, per_sector));
+          sel_bytes += bpr * docs * (1.0 - std::pow(1.0 - s, per_sector));
         }
       }
-      base.select = forced || sel_b < 0.75 * scan_b;
+      const double sel_t = std::max(leaf_b / kBw, docs_all * kSelectDoc) + matches * kGatherDoc + (sel_bytes - leaf_b) / kBw;
+      base.select = forced || sel_t < 0.9 * scan_t;
     }
     if (base.select && base.lds) {
       // gather blocks may add up to ceil(matches / CUs) + 4 x block docs to one LDS table: re-bound the
@@ -2571,11 +2596,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (leaf_slot[sl]) L.filter_bytes += bpr * (double)ls[k].num_docs;
           if (value_slot[sl] && k == 0) L.value_bpr += bpr;
         }
-      // exact capacity: the launch's matching docs (plan-time counts) + at most 3 padding entries per
-      // wave run (one run per 256-doc wave tile)
+      // capacity from the launch's matching docs (plan-time counts): + at most 3 padding entries per
+      // wave run (one run per 256-doc wave tile); a wave's chunk of kSelChunk entries holds at least
+      // kSelChunk - 255 of them before the wave moves on (a run is <= 256 entries), and every wave may
+      // leave one chunk partly unused
       int64_t m = 0;
       for (int si : L.segs) m += seg_matched[si] + 3 * ((segs[si]->num_docs + 255) / 256 + 1);
-      max_sel = std::max<int64_t>(max_sel, m + 64);
+      const int64_t waves = (int64_t)cus * nb * 4;
+      const int64_t chunks = (m + (kSelChunk - 256)) / (kSelChunk - 255) + waves;
+      max_sel = std::max<int64_t>(max_sel, chunks * kSelChunk + 64);
     } else {
       int nb = 0;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||
