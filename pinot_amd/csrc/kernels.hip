@@ -557,7 +557,8 @@ struct RoaringContainer {
 __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const ExpandJob* jobs, int32_t njobs,
                                                                       int64_t total_items) {
   __shared__ uint32_t lbits[2048];
-  __shared__ int32_t bigq[kBlock];
+  constexpr int kPer = 4;  // containers per lane per round: their loads are independent (latency overlap)
+  __shared__ int32_t bigq[kBlock * kPer];
   __shared__ int32_t nbig;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
@@ -572,23 +573,35 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
     if (tid == 0) nbig = 0;
     __syncthreads();
     const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
-    for (int32_t base = g0; base < g1; base += kBlock) {
-      const int32_t ci = base + tid;
-      if (ci < g1) {
-        const RoaringContainer c = J.conts[J.sel[ci]];
-        const uint8_t* p = J.inv + c.offset;
-        if (c.kind == 0 && c.count <= 16) {
-          // every entry loaded before the first LDS atomic: one memory latency per container instead
-          // of one per entry (payloads are 2-byte aligned: every part of the portable format is even)
-          const uint16_t* p16 = reinterpret_cast<const uint16_t*>(p);
-          uint32_t v[16];
+    for (int32_t base = g0; base < g1; base += kBlock * kPer) {
+      // every load of the round first (selected index, descriptor, small-array payload), then the LDS work
+      int32_t si[kPer];
 #pragma unroll
-          for (uint32_t e = 0; e < 16; ++e) v[e] = e < c.count ? p16[e] : 0u;
+      for (int u = 0; u < kPer; ++u) {
+        const int32_t ci = base + u * kBlock + tid;
+        si[u] = ci < g1 ? J.sel[ci] : -1;
+      }
+      RoaringContainer c[kPer];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u)
+        if (si[u] >= 0) c[u] = J.conts[si[u]];
+      uint32_t v[kPer][16];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const bool small = si[u] >= 0 && c[u].kind == 0 && c[u].count <= 16;
+        const uint16_t* p16 = small ? reinterpret_cast<const uint16_t*>(J.inv + c[u].offset) : nullptr;
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e) v[u][e] = small && e < c[u].count ? p16[e] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        if (si[u] < 0) continue;
+        if (c[u].kind == 0 && c[u].count <= 16) {
 #pragma unroll
           for (uint32_t e = 0; e < 16; ++e)
-            if (e < c.count) atomicOr(&lbits[v[e] >> 5], 1u << (v[e] & 31));
+            if (e < c[u].count) atomicOr(&lbits[v[u][e] >> 5], 1u << (v[u][e] & 31));
         } else {
-          bigq[atomicAdd(&nbig, 1)] = J.sel[ci];
+          bigq[atomicAdd(&nbig, 1)] = si[u];
         }
       }
       __syncthreads();
