@@ -1059,7 +1059,7 @@ struct Launch {
   double col_bytes = 0;  // algorithmic bytes of the launch's decoded columns over all its docs
   bool gated = false;    // an inverted-index gate clause: columns are read only where it passes
   // selection-vector plan (late materialisation): select pass over the filter columns, gather pass
-  bool select = false;
+  bool select = false, word_select = false;
   int gather_grid = 1, gather_threads = 256;
   double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
   // partitioned: record size; sampled capacities (strided histogram instead of the count pass)
@@ -2327,9 +2327,18 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       for (int c = 0; c < nclauses; ++c) gated |= gate[c] && has[c];
     }
+    // a filter reading no column (docId bitsets / ranges / constants) selects on 64-doc words
+    bool wordy = np > 0;
+    for (size_t k = 0; k < order.size(); ++k)
+      for (int si = 0; si < n; ++si) {
+        const int kd = hsegs[si].leaves[k].kind;
+        if (kd != LEAF_DOC_BITSET && kd != LEAF_DOC_RANGE && kd != LEAF_CONST) wordy = false;
+      }
+    constexpr double kWordDoc = 0.1e-12;  // word-level select pass, per doc
+    const double sel_doc = wordy ? kWordDoc : kSelectDoc;
     const double scan_t = std::max(scan_b / kBw, docs_all * (gated ? kGatedDoc : kScanDoc));
     const bool forced = sel_env && !strcmp(sel_env, "always");
-    if (forced || std::max(leaf_b / kBw, docs_all * kSelectDoc) < 0.9 * scan_t) {  // the select pass alone could win
+    if (forced || std::max(leaf_b / kBw, docs_all * sel_doc) < 0.9 * scan_t) {  // the select pass alone could win
       if (int rc = probe_matched()) return rc;
       double sel_bytes = leaf_b, matches = 0;
       for (int si = 0; si < n; ++si) {
@@ -2346,8 +2355,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           sel_bytes += bpr * docs * (1.0 - std::pow(1.0 - s, per_sector));
         }
       }
-      const double sel_t = std::max(leaf_b / kBw, docs_all * kSelectDoc) + matches * kGatherDoc + (sel_bytes - leaf_b) / kBw;
+      const double sel_t = std::max(leaf_b / kBw, docs_all * sel_doc) + matches * kGatherDoc + (sel_bytes - leaf_b) / kBw;
       base.select = forced || sel_t < 0.9 * scan_t;
+      base.word_select = base.select && wordy && !env_is("PINOT_AMD_WORD_SELECT", "0");
     }
     if (base.select && base.lds) {
       // gather blocks may add up to ceil(matches / CUs) + 4 x block docs to one LDS table: re-bound the
@@ -2581,6 +2591,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     } else if (jp.select) {
       // select pass: plain 256-thread blocks without LDS; gather pass: the table's block size and LDS
       L.select = true;
+      L.word_select = jp.word_select;
       L.scan_nsub = 1;
       L.gather_threads = jp.lds ? kBlock * jp.scan_nsub : kBlock;
       int nb = 0, ng = 0;
@@ -2601,7 +2612,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // kSelChunk - 255 of them before the wave moves on (a run is <= 256 entries), and every wave may
       // leave one chunk partly unused
       int64_t m = 0;
-      for (int si : L.segs) m += seg_matched[si] + 3 * ((segs[si]->num_docs + 255) / 256 + 1);
+      for (int si : L.segs)  // word-level select: one padded run per 64-doc word with a match
+        m += seg_matched[si] + 3 * (jp.word_select ? std::min<int64_t>(seg_matched[si], (segs[si]->num_docs + 63) / 64 + 16)
+                                                   : (segs[si]->num_docs + 255) / 256 + 1);
       const int64_t waves = (int64_t)cus * nb * 4;
       const int64_t chunks = (m + (kSelChunk - 256)) / (kSelChunk - 255) + waves;
       max_sel = std::max<int64_t>(max_sel, chunks * kSelChunk + 64);
@@ -2804,7 +2817,7 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
   }
   for (const auto& L : r->launches)
     if (L.select) {
-      info += "-select";
+      info += L.word_select ? "-wselect" : "-select";  // wselect: the filter ran on 64-doc words
       break;
     }
   if (r->launches.size() > 1) info += " x" + std::to_string(r->launches.size());

@@ -95,6 +95,9 @@ struct JitPlan {
   // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;
+  // ... whose filter reads no column (docId bitsets / ranges / constants only): the select pass
+  // evaluates the CNF on 64-doc words
+  bool word_select = false;
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);

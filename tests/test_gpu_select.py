@@ -100,3 +100,31 @@ def test_cost_model_picks_select_for_selective_wide_rows(engine, monkeypatch):
         assert ("select" in res.kernel_info()) == expect, (where, res.kernel_info())
         _, og = oracle.execute(q, [bufs])
         assert_same_groups(res.groups(), og, {2})
+
+
+WORD_QUERIES = [
+    "SELECT COUNT(*), SUM(r_long), MAX(r_double), MIN(r_int) FROM t WHERE d1 IN (10, 17, 73) AND ts BETWEEN 5 AND 40",
+    "SELECT d0, COUNT(*), SUM(r_int) FROM t WHERE d1 NOT IN (3, 10) OR ts < 3 GROUP BY d0",
+    "SELECT ts, COUNT(*), SUM(r_double) FROM t WHERE d1 = 24 GROUP BY ts",
+    "SELECT COUNT(*), SUM(r_int) FROM t WHERE d1 IN (10, 17) AND ts > 100",  # nothing matches
+]
+
+
+@pytest.mark.parametrize("qi", range(len(WORD_QUERIES)))
+def test_word_select_vs_oracle(engine, data, monkeypatch, qi):
+    """Filters that read no column (inverted-index bitsets, sorted-index docId ranges, constants) select
+    on 64-doc words: ragged segment sizes (1 .. 131072 docs, partial last words), negation, OR/AND."""
+    monkeypatch.setenv("PINOT_AMD_SELECT", "always")
+    monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
+    bufs, segs = data
+    q = WORD_QUERIES[qi]
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert "wselect" in res.kernel_info(), res.kernel_info()
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    from pinot_amd.query import parse_sql
+    qc = parse_sql(q)
+    fs = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "r_double"}
+    assert_same_groups(res.groups(), og, fs)
+    res.execute_again()
+    assert_same_groups(res.groups(), og, fs)
