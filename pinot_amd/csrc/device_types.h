@@ -155,6 +155,8 @@ struct DevQuery {
   unsigned long long* sel_entries;
   unsigned long long* sel_count;
   int64_t sel_cap;
+  int32_t sel_chunk;     // vector entries a select wave reserves at a time (planner: from the expected matches)
+  int32_t sel_pad;
 };
 
 }  // namespace pamd

@@ -2607,17 +2607,24 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (leaf_slot[sl]) L.filter_bytes += bpr * (double)ls[k].num_docs;
           if (value_slot[sl] && k == 0) L.value_bpr += bpr;
         }
-      // capacity from the launch's matching docs (plan-time counts): + at most 3 padding entries per
-      // wave run (one run per 256-doc wave tile); a wave's chunk of kSelChunk entries holds at least
-      // kSelChunk - 255 of them before the wave moves on (a run is <= 256 entries), and every wave may
-      // leave one chunk partly unused
-      int64_t m = 0;
-      for (int si : L.segs)  // word-level select: one padded run per 64-doc word with a match
-        m += seg_matched[si] + 3 * (jp.word_select ? std::min<int64_t>(seg_matched[si], (segs[si]->num_docs + 63) / 64 + 16)
-                                                   : (segs[si]->num_docs + 255) / 256 + 1);
+      // Vector chunk a wave reserves at a time: about twice the matches a wave expects (plan-time
+      // counts), a power of two in [512, 1024] for the tile-level select (a run of up to 256 entries
+      // must fit a chunk) or [64, 1024] for the word-level one (runs split across chunks): few
+      // reservations on the shared counter, little padding for the gather to read when matches are rare.
+      int64_t m = 0, mt = 0;
+      for (int si : L.segs) {  // + padding: one run per 256-doc wave tile, or per lane's 256 docs
+        mt += seg_matched[si];
+        m += seg_matched[si] + 3 * std::min<int64_t>(seg_matched[si], (segs[si]->num_docs + 255) / 256 + 1);
+      }
       const int64_t waves = (int64_t)cus * nb * 4;
-      const int64_t chunks = (m + (kSelChunk - 256)) / (kSelChunk - 255) + waves;
-      max_sel = std::max<int64_t>(max_sel, chunks * kSelChunk + 64);
+      int64_t chunk = jp.word_select ? 64 : 512;
+      while (chunk < 1024 && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
+      L.q.sel_chunk = (int32_t)chunk;
+      // a tile-level chunk holds >= chunk - 255 entries before the wave takes another; a word-level chunk
+      // is filled; every wave may leave its last chunk partly unused
+      const int64_t per_chunk = jp.word_select ? chunk : chunk - 255;
+      const int64_t chunks = (m + per_chunk - 1) / per_chunk + waves + 1;
+      max_sel = std::max<int64_t>(max_sel, chunks * chunk + 64);
     } else {
       int nb = 0;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||

@@ -12,7 +12,6 @@ namespace pamd {
 
 constexpr int kPartSub = 4;  // partition count / scatter blocks: 4 x 256 threads (one block per CU)
 constexpr int kPartCountRatio = 2;  // count-pass blocks per scatter-pass block (count needs little LDS)
-constexpr int kSelChunk = 1024;     // selection-vector entries a select wave reserves at a time
 
 struct JitSlot {
   int enc;       // ENC_* (the same in every segment of the batch)
