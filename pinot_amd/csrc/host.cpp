@@ -1060,6 +1060,7 @@ struct Launch {
   bool gated = false;    // an inverted-index gate clause: columns are read only where it passes
   // selection-vector plan (late materialisation): select pass over the filter columns, gather pass
   bool select = false, word_select = false;
+  size_t shmem_sets = 0;  // LDS dictId sets of the scan / select pass (JitLeaf::lds_words)
   int gather_grid = 1, gather_threads = 256;
   double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
   // partitioned: record size; sampled capacities (strided histogram instead of the count pass)
@@ -1564,7 +1565,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   void* args[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
   if (L.select) {  // select pass (filter columns -> selection vector), then the gather-aggregate pass
     HIP_OK(hipMemsetAsync(L.q.sel_count, 0, 16, st));
-    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, (unsigned)L.shmem_sets, st, args, nullptr));
     if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
       unsigned long long ctr[2];
       HIP_OK(hipMemcpyAsync(ctr, L.q.sel_count, 16, hipMemcpyDeviceToHost, st));
@@ -2472,6 +2473,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         if (jl.slot >= 0) small_sets &= d.cols[jl.slot].card < 64 * 32;
       }
       jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
+      // larger dictId sets (<= 4096 words) are read from LDS, not from global memory per doc, by the
+      // 256-thread blocks of non-partitioned plans (fused scans with nsub 1, every select pass)
+      if (!jl.bits_regs && jl.slot >= 0 && (jl.kinds & (1u << LEAF_DICT_SET)) && !jp.partitioned &&
+          (jp.scan_nsub == 1 || jp.select) && !env_is("PINOT_AMD_LDS_SETS", "0")) {
+        int64_t w = 0;
+        for (auto& d : ls) w = std::max<int64_t>(w, (d.cols[jl.slot].card >> 5) + 1);
+        int64_t used = 0;
+        for (auto& o : jp.leaves) used += o.lds_words;
+        w = (w + 3) & ~(int64_t)3;
+        if (w <= 4096 && used + w <= 8192) jl.lds_words = (int)w;
+      }
       jp.leaves.push_back(jl);
     }
     {  // pipeline depth: ~4 KiB in flight per wave (256 docs x bytes per row)
@@ -2522,6 +2534,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
     L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : 0;
+    for (const JitLeaf& jl : jp.leaves) L.shmem_sets += (size_t)jl.lds_words * 4;
+    if (!jp.select) L.shmem += L.shmem_sets;  // a select pass has no table: its sets start at 0
     int per_cu = 1;
     if (jp.partitioned) {
       JitPlan ja = jp;  // companion direct-atomic scan for batches where the filter keeps few docs
@@ -2595,7 +2609,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.scan_nsub = 1;
       L.gather_threads = jp.lds ? kBlock * jp.scan_nsub : kBlock;
       int nb = 0, ng = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, L.shmem_sets) != hipSuccess || nb < 1) nb = 1;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
           ng < 1)
         ng = 1;

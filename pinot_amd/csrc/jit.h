@@ -25,6 +25,9 @@ struct JitLeaf {
   int negate;
   uint32_t kinds;  // bit k set: some segment resolves this predicate to LEAF kind k
   int bits_regs = 0;  // dictId set of <= 64 words in every segment: held one word per lane
+  // dictId set of <= lds_words 32-bit words in every segment (too large for lane registers): copied
+  // into LDS when the block's segment changes (256-thread blocks only: the segment is block-uniform)
+  int lds_words = 0;
 };
 // value an accumulator reads: a column slot, or a binary arithmetic expression of two slots
 // (EXPR_MUL / SUB / ADD: Pinot's times / minus / plus transforms)

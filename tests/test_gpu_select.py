@@ -128,3 +128,30 @@ def test_word_select_vs_oracle(engine, data, monkeypatch, qi):
     assert_same_groups(res.groups(), og, fs)
     res.execute_again()
     assert_same_groups(res.groups(), og, fs)
+
+
+_D2_SET = ", ".join(str(7 * v + 3) for v in range(0, 9000, 29))  # 311 values of the 9000-entry dictionary
+SET_QUERIES = [
+    f"SELECT COUNT(*), SUM(r_long), MAX(r_double) FROM t WHERE d2 IN ({_D2_SET})",
+    f"SELECT d1, COUNT(*), SUM(r_int) FROM t WHERE d2 NOT IN ({_D2_SET}) AND d0 < 2000 GROUP BY d1",
+    f"SELECT d0, COUNT(*), MIN(r_long) FROM t WHERE d2 IN ({_D2_SET}) OR r_int > 900000 GROUP BY d0",
+]
+
+
+@pytest.mark.parametrize("sel", ["never", "always"])
+@pytest.mark.parametrize("qi", range(len(SET_QUERIES)))
+def test_lds_dictid_sets_vs_oracle(engine, data, monkeypatch, qi, sel):
+    """IN / NOT IN over a 9000-entry dictionary (282 bitmap words: above the lane-register tables) read
+    from an LDS copy of the segment's dictId set, in the fused scan (aggregation only, LDS table, HBM
+    table) and in the select pass, across segment changes inside a block's tile range."""
+    monkeypatch.setenv("PINOT_AMD_SELECT", sel)
+    monkeypatch.setenv("PINOT_AMD_PARTITIONED", "0")
+    bufs, segs = data
+    q = SET_QUERIES[qi]
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    from pinot_amd.query import parse_sql
+    qc = parse_sql(q)
+    fs = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "r_double"}
+    assert_same_groups(res.groups(), og, fs)
