@@ -2510,7 +2510,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       while (cap >= 4 && jit_scatter_lds(jp, cap) > (size_t)lds_max) --cap;
       jp.stage_cap = cap >= 4 ? cap : 0;
       if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
-      jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 50)));
+      jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
     }
     {  // algorithmic bytes: each decoded column once (fixed-bit at its width, raw at its value width)
       for (size_t k = 0; k < L.segs.size(); ++k)
