@@ -223,8 +223,9 @@ class QueryResult:
         return bool(out.value)
 
     def kernel_info(self) -> str:
-        """'jit' when the query-specialised kernel runs ('jit-partitioned' for the partitioned
-        high-cardinality GROUP BY), else 'aot: <reason>'."""
+        """The device plan: 'jit' (fused scan), 'jit-select' / 'jit-wselect' (selection vector; the
+        filter on 4-doc tiles / 64-doc bitset words), 'jit-partitioned', 'jit-hash', 'jit-hash-trim';
+        ' xN' when the batch ran as N shape launches."""
         return lib().pinot_amd_result_kernel_info(self._h).decode()
 
     def last_kernel_ms(self) -> float:
