@@ -117,6 +117,10 @@ struct ExpandJob {
   int64_t sel_begin;           // prefix of nsel over the plan's jobs
   int64_t item_begin;          // prefix of nchunks over the plan's jobs (work items)
   int32_t nsel, nchunks;
+  // the selected containers' descriptors packed in the sel order (byte offset | min(count, 65535) << 32
+  // | kind << 48), built once per plan: one load per container instead of sel -> directory; nullptr
+  // when the inverted-index buffer is 4 GiB or larger
+  const unsigned long long* psel;
 };
 
 // One compressed chunk of a raw forward index (BaseChunkForwardIndexWriter layout), decoded on the

@@ -55,6 +55,7 @@ hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* 
 hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
                                  int32_t* out, hipStream_t st);
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
+hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, unsigned long long* out, hipStream_t st);
 hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
                                     int64_t* d_part_begin, hipStream_t st);
 hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int mode, int64_t stride, double scale,
@@ -1087,6 +1088,7 @@ struct pinot_amd_result {
     int32_t nsel, nchunks;
     int64_t num_docs;
     double alg_bytes;  // selected bitmap payloads + the dense bitset written and read once
+    DevBuf* psel = nullptr;  // packed descriptors in sel order (ExpandJob::psel), or none
   };
   std::vector<InvLeaf> inv_leaves;
   DevBuf d_expand_jobs;        // one ExpandJob per inv_leaves entry (batched clear + expand launches)
@@ -1402,6 +1404,14 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     for (int32_t d : ids) sel_bytes += (double)(c.inv_bytes[d + 1] - c.inv_bytes[d]);
     r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), nchunks, seg->num_docs,
                              sel_bytes + 2.0 * (double)((seg->num_docs + 7) / 8)});
+    if (!sel.empty() && c.inv.n < ((size_t)1 << 32)) {  // packed descriptors, built once per plan
+      auto pb = std::make_unique<DevBuf>();
+      rc = pb->alloc(sel.size() * 8);
+      if (rc) return rc;
+      HIP_OK(launch_pack_sel(c.inv_conts.p, (const int32_t*)sb->p, (int64_t)sel.size(), (unsigned long long*)pb->p, st));
+      r->inv_leaves.back().psel = pb.get();
+      r->owned.push_back(std::move(pb));
+    }
     r->owned.push_back(std::move(gb));
     L->kind = LEAF_DOC_BITSET;
     L->bits = (const uint32_t*)bs->p;
@@ -2095,6 +2105,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       J.sel_begin = total;
       J.nsel = il.nsel;
       J.grp = (const int32_t*)il.grp->p;
+      J.psel = il.psel ? (const unsigned long long*)il.psel->p : nullptr;
       J.item_begin = items;
       J.nchunks = il.nchunks;
       total += il.nsel;

@@ -549,6 +549,29 @@ struct RoaringContainer {
   uint64_t offset;   // byte offset of the container payload inside the staged inverted index
 };
 
+// descriptor of the container at position ci of a job's selection
+__device__ __forceinline__ RoaringContainer expand_desc(const ExpandJob& J, int32_t ci) {
+  if (J.psel) {
+    const unsigned long long d = J.psel[ci];
+    RoaringContainer c;
+    c.key = 0u;
+    c.kind = (uint32_t)(d >> 48);
+    c.count = (uint32_t)((d >> 32) & 0xFFFFu);
+    c.pad = 0u;
+    c.offset = d & 0xFFFFFFFFull;
+    return c;
+  }
+  return J.conts[J.sel[ci]];
+}
+
+// Plan time: pack the selected containers' descriptors in sel order (ExpandJob::psel)
+__global__ void pack_sel_kernel(const RoaringContainer* conts, const int32_t* sel, int64_t n, unsigned long long* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const RoaringContainer c = conts[sel[i]];
+    out[i] = c.offset | ((unsigned long long)min(c.count, 65535u) << 32) | ((unsigned long long)c.kind << 48);
+  }
+}
+
 // Batched expansion: every (segment, inverted-index leaf) of a plan is one ExpandJob; a work item
 // is one 65536-doc chunk of one job. A block builds its chunk's 8 KiB of bitset in LDS from the
 // chunk's selected containers (LDS atomics, no global atomics), then writes all 1024 words once
@@ -575,16 +598,14 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
     const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
     for (int32_t base = g0; base < g1; base += kBlock * kPer) {
       // every load of the round first (selected index, descriptor, small-array payload), then the LDS work
-      int32_t si[kPer];
+      int32_t si[kPer];  // position in the job's sel order, -1: none
+      RoaringContainer c[kPer];
 #pragma unroll
       for (int u = 0; u < kPer; ++u) {
         const int32_t ci = base + u * kBlock + tid;
-        si[u] = ci < g1 ? J.sel[ci] : -1;
+        si[u] = ci < g1 ? ci : -1;
+        if (si[u] >= 0) c[u] = expand_desc(J, ci);
       }
-      RoaringContainer c[kPer];
-#pragma unroll
-      for (int u = 0; u < kPer; ++u)
-        if (si[u] >= 0) c[u] = J.conts[si[u]];
       uint32_t v[kPer][16];
 #pragma unroll
       for (int u = 0; u < kPer; ++u) {
@@ -607,7 +628,7 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
       __syncthreads();
       const int nb = nbig;
       for (int qi = wave; qi < nb; qi += kBlock / 64) {
-        const RoaringContainer c = J.conts[bigq[qi]];
+        const RoaringContainer c = expand_desc(J, bigq[qi]);
         const uint8_t* p = J.inv + c.offset;
         if (c.kind == 1) {
           for (int i = lane; i < 1024; i += 64) {
@@ -1027,6 +1048,13 @@ hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int
   if (P <= 0) return hipSuccess;
   hipLaunchKernelGGL(allot_local_kernel, dim3((unsigned)P), dim3(256), 0, st, d_hist, G, mode, stride, scale, d_out, d_ptot);
   hipLaunchKernelGGL(allot_base_kernel, dim3((unsigned)P), dim3(256), 0, st, d_ptot, P, G, limit, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, unsigned long long* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_sel_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const RoaringContainer*)conts, sel, n, out);
   return hipGetLastError();
 }
 
