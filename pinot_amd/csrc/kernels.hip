@@ -541,6 +541,8 @@ __global__ void bitset_compact_kernel(const uint64_t* bits, int64_t nwords, cons
 // Inverted index expansion: one block per (dictId, container) entry of a container directory
 // built at staging time. Sets the container's docs in the dense bitset (atomicOr: containers of
 // different dictIds share 64-bit words).
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));  // 16-byte load, dword-aligned
+
 struct RoaringContainer {
   uint32_t key;      // high 16 bits of the docIds
   uint32_t kind;     // 0 array, 1 bitmap, 2 run
@@ -606,13 +608,28 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
         si[u] = ci < g1 ? ci : -1;
         if (si[u] >= 0) c[u] = expand_desc(J, ci);
       }
+      // a small array's <= 16 two-byte entries with 3 dword-aligned 16-byte loads (48 bytes from the
+      // dword holding the first entry; the staged buffer's zero padding keeps the tail in bounds)
       uint32_t v[kPer][16];
 #pragma unroll
       for (int u = 0; u < kPer; ++u) {
         const bool small = si[u] >= 0 && c[u].kind == 0 && c[u].count <= 16;
-        const uint16_t* p16 = small ? reinterpret_cast<const uint16_t*>(J.inv + c[u].offset) : nullptr;
+        uint32_t w[12];
+        const uint32_t odd = (uint32_t)(c[u].offset >> 1) & 1u;  // entry 0 in the dword's high half
+        if (small) {
+          const u32x4a4* p4 = reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull));
+          const u32x4a4 a = p4[0], b = p4[1], d = p4[2];
+          w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y;
+          w[6] = b.z; w[7] = b.w; w[8] = d.x; w[9] = d.y; w[10] = d.z; w[11] = d.w;
+        }
 #pragma unroll
-        for (uint32_t e = 0; e < 16; ++e) v[u][e] = small && e < c[u].count ? p16[e] : 0u;
+        for (uint32_t e = 0; e < 16; ++e) {
+          // 16-bit entry e is halfword e + odd of the aligned dwords (compile-time indices: e is unrolled)
+          const uint32_t x0 = (e & 1u) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
+          const uint32_t x1 = ((e + 1) & 1u) ? (w[(e + 1) >> 1] >> 16) : (w[(e + 1) >> 1] & 0xFFFFu);
+          const uint32_t x = odd ? x1 : x0;
+          v[u][e] = small && e < c[u].count ? x : 0u;
+        }
       }
 #pragma unroll
       for (int u = 0; u < kPer; ++u) {
