@@ -2625,6 +2625,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
           ng < 1)
         ng = 1;
+      // select blocks per CU: fewer, longer-running waves reserve vector chunks on the shared counter
+      // fewer times (same-address atomics serialise at the memory side). The word-level select reads
+      // little per doc and is bound by those reservations: 4 per CU (swept 1/2/4/8: 1 % inverted
+      // 1.42/1.31/1.27/1.38 ms); the tile-level select needs its occupancy (2 per CU: SSB Q1.2 0.65 -> 0.92 ms)
+      if (jp.word_select) nb = std::min(nb, 4);
+      if (const char* e = getenv("PINOT_AMD_SELECT_PER_CU")) nb = std::max(1, std::min(nb, atoi(e)));
       per_cu = nb;
       L.gather_grid = cus * ng;
       for (size_t k = 0; k < L.segs.size(); ++k)
@@ -2634,8 +2640,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (value_slot[sl] && k == 0) L.value_bpr += bpr;
         }
       // Vector chunk a wave reserves at a time: about twice the matches a wave expects (plan-time
-      // counts), a power of two in [512, 1024] for the tile-level select (a run of up to 256 entries
-      // must fit a chunk) or [64, 1024] for the word-level one (runs split across chunks): few
+      // counts), a power of two in [512, 4096] for the tile-level select (a run of up to 256 entries
+      // must fit a chunk) or [64, 4096] for the word-level one (runs split across chunks): few
       // reservations on the shared counter, little padding for the gather to read when matches are rare.
       int64_t m = 0, mt = 0;
       for (int si : L.segs) {  // + padding: one run per 256-doc wave tile, or per lane's 256 docs
@@ -2644,7 +2650,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       const int64_t waves = (int64_t)cus * nb * 4;
       int64_t chunk = jp.word_select ? 64 : 512;
-      while (chunk < 1024 && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
+      while (chunk < 4096 && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
       L.q.sel_chunk = (int32_t)chunk;
       // a tile-level chunk holds >= chunk - 255 entries before the wave takes another; a word-level chunk
       // is filled; every wave may leave its last chunk partly unused
