@@ -529,6 +529,82 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
     return total, groups
 
 
+def cpu_plan(query, seg: SegmentBuffers, use_inverted: bool = True):
+    """The per-doc C work of execute() for ONE segment, set up once: returns a zero-argument callable
+    that re-runs the inverted-index leaves' bitmap expansion (BitmapBasedFilterOperator), the filter
+    (ScanBasedFilterOperator / And / Or) and the aggregation or group-by (AggregationOperator /
+    DefaultGroupByExecutor) in pinot_oracle.c and returns the matched-doc count. Predicate resolution,
+    buffer setup and the Python conversion of the groups stay outside, so bench.py's cpu_baseline
+    times what a Pinot server does per doc and per segment, not this module's Python."""
+    qc = parse_sql(query) if isinstance(query, str) else query
+    assert not any(a.func == "DISTINCTCOUNT" for a in qc.aggregations), "cpu_plan: no DISTINCTCOUNT"
+    os_ = OracleSegment(seg)
+    n = seg.num_docs
+    L = lib()
+    leaves, nl = os_.leaves(qc, use_inverted) if qc.cnf else (None, 0)
+    inv_steps = []  # (inverted bytes, cardinality, dictIds, the leaf's bitset) of each inverted-index leaf
+    nwords = (n + 63) // 64 + 1
+    for i, (p, _neg) in enumerate(pn for clause in qc.cnf for pn in clause):
+        if leaves[i].kind == DOC_BITSET:
+            cb = seg.columns[p.column]
+            idarr = np.array(_dict_positions(cb, p.values), dtype=np.int32)
+            inv = np.frombuffer(cb.inverted, dtype=np.uint8)
+            bits = np.ctypeslib.as_array(C.cast(leaves[i].doc_bitset, C.POINTER(C.c_uint64)), shape=(nwords,))
+            inv_steps.append((inv, cb.cardinality, idarr, bits))
+    fbits = np.zeros((n + 63) // 64 + 1, dtype=np.uint64)
+    nat = []
+    for a in qc.aggregations:
+        if a.func == "AVG":
+            nat += [("SUM", a.column, a.expr), ("COUNT", "*", None)]
+        elif a.func == "MINMAXRANGE":
+            nat += [("RMIN", a.column, a.expr), ("RMAX", a.column, a.expr)]
+        else:
+            nat.append((a.func, a.column, a.expr))
+    if not nat:
+        nat.append(("COUNT", "*", None))
+
+    def oagg(f, c, e):
+        if c == "*":
+            return OAgg(AGG[f], -1, 0, -1)
+        if e is None or e[0] == "COL":
+            return OAgg(AGG[f], os_.index[c if e is None else e[1]], 0, -1)
+        return OAgg(AGG[f], os_.index[e[1]], EXPR[e[0]], os_.index[e[2]])
+    aggs = (OAgg * len(nat))(*[oagg(f, c, e) for f, c, e in nat])
+    ng = len(qc.group_by)
+    gcols = np.array([os_.group_col(g) for g in qc.group_by] or [0], dtype=np.int32)
+    cap = 1
+    if ng:  # groups <= min(docs, key space, numGroupsLimit)
+        space = 1
+        for c in gcols:
+            space *= max(int(os_.cols[int(c)].cardinality), 1)
+        cap = max(1, min(n, space, qc.num_groups_limit))
+    keys = np.zeros(cap * max(ng, 1), dtype=np.int32)
+    vals = np.zeros(cap * len(nat), dtype=np.float64)
+    vali = np.zeros(cap * len(nat), dtype=np.int64)
+    valh = np.zeros(cap * len(nat), dtype=np.int64)
+    reached = C.c_int32(0)
+
+    def run() -> int:
+        for inv, card, idarr, bits in inv_steps:
+            bits[:] = 0
+            rc = L.oracle_inverted_to_bitset(_ptr(inv), card, _ptr(idarr), len(idarr), _ptr(bits), n)
+            assert rc == 0, rc
+        if qc.cnf:
+            cnt = int(L.oracle_filter(os_.cols, n, leaves, nl, _ptr(fbits)))
+            bptr = _ptr(fbits)
+        else:
+            cnt, bptr = n, None
+        if ng:
+            r = L.oracle_group_by(os_.cols, n, bptr, _ptr(gcols), ng, aggs, len(nat), qc.num_groups_limit, cap,
+                                  _ptr(keys), _ptr(vals), _ptr(vali), _ptr(valh), C.byref(reached))
+            assert r >= 0, r
+        else:
+            L.oracle_aggregate(os_.cols, n, bptr, aggs, len(nat), _ptr(vals), _ptr(vali), _ptr(valh))
+        return cnt
+    run.keep = (os_, leaves, inv_steps)
+    return run
+
+
 def _distinct_count(qc: QueryContext, segments, use_inverted: bool, stats):
     """DistinctCountAggregationFunction (aggregate / aggregateGroupBySV: add each matching doc's value
     to its group's set; merge = union; final = size), restated directly over the docs: the filter's

@@ -105,7 +105,10 @@ def highcard_segment(name: str, num_docs: int, seed: int, device: str = "cuda") 
 # Pinot keeps every group (its default, 100000, would trim)
 HIGHCARD_QUERY = ("SET numGroupsLimit = 2000000; SELECT dimA, dimB, COUNT(*), SUM(metInt), MIN(metLong), "
                   "MAX(metDouble) FROM highCard WHERE metInt < 900 GROUP BY dimA, dimB")
-HIGHCARD_BYTES_PER_ROW = 2 * S.num_bits_per_value(HC_CARD - 1) / 8.0 + 4 + 8 + 8
+# the same query as Pinot runs it by default (numGroupsLimit 100000 < 1M keys per segment): each segment
+# admits only the first 100000 groups it sees (DictionaryBasedGroupKeyGenerator.java:351-363)
+HIGHCARD_DEFAULT_QUERY = HIGHCARD_QUERY.split(";", 1)[1].strip()
+HIGHCARD_BYTES_PER_ROW =2 * S.num_bits_per_value(HC_CARD - 1) / 8.0 + 4 + 8 + 8
 
 
 # ---------------------------------------------------------------------------------------------
