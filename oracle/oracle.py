@@ -20,8 +20,11 @@ from typing import Dict, List, Sequence
 
 import numpy as np
 
-from pinot_amd.query import (JavaDouble, QueryContext, canonical_key, distinct_value, merge_partial, parse_sql, reduce_rows,
-                             split_distinct_count)
+import dataclasses
+
+from pinot_amd.query import Aggregation, QueryContext, parse_sql  # the SQL front end only: no arithmetic
+from oracle_reduce import JDouble, identity_key, java_identity, merge
+from oracle_reduce import rows as reduce_rows
 from pinot_amd.segment import (DOUBLE, FLOAT, INT, LONG, STRING, ColumnBuffers, SegmentBuffers,
                                parse_raw_fwd_header)
 
@@ -87,6 +90,8 @@ def lib():
         L.oracle_bitset_to_doc_ids.restype = I64
         L.oracle_bitset_to_doc_ids.argtypes = [P, I64, P]
         L.oracle_aggregate.argtypes = [C.POINTER(OColumn), I64, P, C.POINTER(OAgg), C.c_int32, P, P, P]
+        L.oracle_set_literal_int_sum.argtypes = [C.c_int32]
+        L.oracle_literal_int_sum.restype = C.c_int32
         L.oracle_group_by.restype = I64
         L.oracle_group_by.argtypes = [C.POINTER(OColumn), I64, P, P, C.c_int32, C.POINTER(OAgg), C.c_int32, I64, I64,
                                       P, P, P, P, P]
@@ -443,16 +448,25 @@ class OracleSegment:
         for g, d in zip(group_by, dict_ids):
             cb = self.seg.columns[g]
             v = self._raw_groups[g][1][int(d)] if g in self._raw_groups else cb.dict_values[int(d)]
-            out.append(v if cb.stored_type == STRING else (JavaDouble(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
+            out.append(v if cb.stored_type == STRING else (JDouble(v) if cb.stored_type in (FLOAT, DOUBLE) else int(v)))
         return tuple(out)
 
 
-def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True, stats: dict = None):
+def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True, stats: dict = None,
+            literal_int_sum: bool = False):
     """Run a query over segments on the CPU oracle: returns (num_docs_matched, groups) where groups
     maps key tuple -> intermediate results per aggregation (AVG as (sum, count)), combined across
     segments with AggregationFunction.merge semantics (GroupByCombineOperator's upsert by key).
-    stats, when given, receives 'num_groups_limit_reached' (any segment's GroupByOperator flag)."""
+    stats, when given, receives 'num_groups_limit_reached' (any segment's GroupByOperator flag).
+    literal_int_sum: integer SUMs accumulate in double in doc order and merge as doubles in segment
+    order, the reference's own arithmetic (SumAggregationFunction); default: exact, rounded once."""
     qc = parse_sql(query) if isinstance(query, str) else query
+    if literal_int_sum:
+        lib().oracle_set_literal_int_sum(1)
+        try:
+            return execute(qc, segments, use_inverted, stats)
+        finally:
+            lib().oracle_set_literal_int_sum(0)
     if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):
         return _distinct_count(qc, segments, use_inverted, stats)
     if stats is not None:
@@ -490,7 +504,7 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
                 return OAgg(AGG[f], os_.index[c if e is None else e[1]], 0, -1)
             return OAgg(AGG[f], os_.index[e[1]], EXPR[e[0]], os_.index[e[2]])
         aggs = (OAgg * len(nat))(*[oagg(f, c, e) for f, c, e in nat])
-        int_sum = [f == "SUM" and _is_int_value(seg, c, e) for f, c, e in nat]
+        int_sum = [f == "SUM" and _is_int_value(seg, c, e) and not _literal() for f, c, e in nat]
         bptr = _ptr(bits) if bits is not None else None
         if qc.group_by:
             cap = max(cnt, 1)
@@ -519,7 +533,7 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
             seg_groups = {(): _parts(qc, slots, nat, vals, vali, valh, int_sum)}
         for k, parts in seg_groups.items():
             if k in groups:
-                groups[k] = [merge_partial(a.func, x, y) for a, x, y in zip(qc.aggregations, groups[k], parts)]
+                groups[k] = [merge(a.func, x, y) for a, x, y in zip(qc.aggregations, groups[k], parts)]
             else:
                 groups[k] = parts
     # integer SUM partials were carried as exact Python ints through the combine: round once
@@ -609,9 +623,10 @@ def _distinct_count(qc: QueryContext, segments, use_inverted: bool, stats):
     """DistinctCountAggregationFunction (aggregate / aggregateGroupBySV: add each matching doc's value
     to its group's set; merge = union; final = size), restated directly over the docs: the filter's
     matching docs, their group-by values and their DISTINCTCOUNT column values, with value identity
-    as the fastutil sets have it (query.distinct_value). The other aggregations come from the query
+    as the fastutil sets have it (oracle_reduce.java_identity). The other aggregations come from the query
     without its DISTINCTCOUNTs, whose groups are the groups of the query."""
-    base, _ = split_distinct_count(qc)
+    base = dataclasses.replace(qc, aggregations=[a for a in qc.aggregations if a.func != "DISTINCTCOUNT"] or
+                               [Aggregation("COUNT", "*")], order_by=[])
     total, bg = execute(base, segments, use_inverted, stats)
     dc = [i for i, a in enumerate(qc.aggregations) if a.func == "DISTINCTCOUNT"]
     sets = {i: {} for i in dc}
@@ -628,8 +643,8 @@ def _distinct_count(qc: QueryContext, segments, use_inverted: bool, stats):
             vals = os_.values(qc.aggregations[i].column)[docs].tolist()
             s = sets[i]
             for d in range(len(docs)):
-                k = canonical_key(tuple(kc[d] for kc in keys))
-                s.setdefault(k, set()).add(distinct_value(vals[d]))
+                k = identity_key(tuple(kc[d] for kc in keys))
+                s.setdefault(k, set()).add(java_identity(vals[d]))
     rest = [j for j, a in enumerate(qc.aggregations) if a.func != "DISTINCTCOUNT"]
     out = {}
     for key, parts in bg.items():
@@ -637,9 +652,13 @@ def _distinct_count(qc: QueryContext, segments, use_inverted: bool, stats):
         for j, p in zip(rest, parts):
             full[j] = p
         for i in dc:
-            full[i] = frozenset(sets[i].get(canonical_key(key), ()))
+            full[i] = frozenset(sets[i].get(identity_key(key), ()))
         out[key] = full
     return total, out
+
+
+def _literal() -> bool:
+    return bool(lib().oracle_literal_int_sum())
 
 
 def _is_int_value(seg: SegmentBuffers, column, expr) -> bool:

@@ -1,0 +1,106 @@
+"""Combine / broker-reduce restatement for the CPU oracle. TEST INFRASTRUCTURE ONLY.
+
+Restated from the reference independently of pinot_amd.query (the product's host mirror), so the
+oracle's cross-segment combine and its final rows do not share code with what they check:
+
+* merge(): AggregationFunction.merge of each function, null handling disabled
+  (pinot-core/.../query/aggregation/function/): COUNT `a + b` (CountAggregationFunction.java:193-195);
+  SUM / SUMLONG `a + b` (SumAggregationFunction.merge); MIN `a < b ? a : b`
+  (MinAggregationFunction.java:353-367) and MAX `a > b ? a : b` (MaxAggregationFunction.java:353-367) —
+  Java's comparison order, so a NaN on the left loses and on the right wins; AVG AvgPair sums
+  (AvgAggregationFunction.java:271-285); MINMAXRANGE MinMaxRangePair.apply with < / >
+  (MinMaxRangeAggregationFunction.java:278-292); DISTINCTCOUNT set union.
+* final(): extractFinalResult — AVG sum / count, DEFAULT_FINAL_RESULT (-inf) when count is 0
+  (AvgAggregationFunction.java:306-316); MINMAXRANGE max - min (:313-318); DISTINCTCOUNT set size.
+* rows(): GroupByDataTableReducer's final rows: group values then final results, ORDER BY applied
+  stably right to left (the comparator chain of the select list), LIMIT (default 10).
+* Value identity of group keys and DISTINCTCOUNT elements: Double.doubleToLongBits /
+  Float.floatToIntBits (every NaN one value, -0.0 != 0.0), as the fastutil maps and sets compare.
+
+Only the SQL parser (pinot_amd.query.parse_sql: text -> QueryContext) is shared with the product; it
+does no arithmetic.
+"""
+from __future__ import annotations
+
+import math
+import struct
+
+_NAN_BITS = 0x7FF8000000000000
+
+
+def java_identity(v):
+    """Value identity in a group key / DISTINCTCOUNT set (doubleToLongBits for floating values)."""
+    if isinstance(v, float) or type(v).__name__ in ("float64", "float32"):
+        f = float(v)
+        return ("f", _NAN_BITS if math.isnan(f) else struct.unpack("<q", struct.pack("<d", f))[0])
+    return v
+
+
+def identity_key(key) -> tuple:
+    return tuple(java_identity(v) for v in key)
+
+
+class JDouble(float):
+    """A FLOAT/DOUBLE group-key value that compares and hashes by Java's Double.equals identity."""
+    __slots__ = ()
+
+    def __eq__(self, other):
+        if isinstance(other, float):
+            return java_identity(float(self)) == java_identity(float(other))
+        return float.__eq__(self, other)
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    def __hash__(self):
+        return hash(_NAN_BITS) if math.isnan(self) else float.__hash__(self)
+
+    def __repr__(self):
+        return float.__repr__(self)
+
+
+def merge(func: str, a, b):
+    """AggregationFunction.merge(a, b) (a: the combined result so far, b: the next segment's)."""
+    if func in ("COUNT", "SUM", "SUMLONG"):
+        return a + b
+    if func == "MIN":
+        return a if a < b else b
+    if func == "MAX":
+        return a if a > b else b
+    if func == "AVG":
+        return (a[0] + b[0], a[1] + b[1])
+    if func == "MINMAXRANGE":
+        mn = b[0] if b[0] < a[0] else a[0]
+        mx = b[1] if b[1] > a[1] else a[1]
+        return (mn, mx)
+    if func == "DISTINCTCOUNT":
+        return a | b
+    raise ValueError(func)
+
+
+def final(func: str, partial):
+    """AggregationFunction.extractFinalResult."""
+    if func == "AVG":
+        s, c = partial
+        return s / c if c else float("-inf")
+    if func == "MINMAXRANGE":
+        return partial[1] - partial[0]
+    if func == "DISTINCTCOUNT":
+        return len(partial)
+    return partial
+
+
+def rows(qc, groups: dict) -> list:
+    """Final rows: (group values..., final results...), ORDER BY then LIMIT."""
+    out = [tuple(k) + tuple(final(a.func, p) for a, p in zip(qc.aggregations, parts)) for k, parts in groups.items()]
+    names = [g.lower() for g in qc.group_by] + [a.name.lower() for a in qc.aggregations]
+    alt = [g.lower() for g in qc.group_by] + [f"{a.func.lower()}({a.column})".lower() for a in qc.aggregations]
+    for expr, asc in reversed(qc.order_by):
+        e = expr.lower()
+        hits = [i for i in range(len(names)) if e in (names[i], alt[i])]
+        if not hits:
+            raise ValueError(f"ORDER BY {expr} not in select list")
+        i = hits[-1]
+        out.sort(key=lambda r: r[i], reverse=not asc)
+    return out[: qc.limit]

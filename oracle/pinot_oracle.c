@@ -477,6 +477,18 @@ int64_t oracle_bitset_to_doc_ids(const uint64_t* bitset, int64_t num_docs, int32
 
 /* ------------------------------------------------------------------ aggregation */
 
+/* Integer SUM mode. 0 (default): the exact 128-bit integer sum, rounded to double once — what the
+ * device computes, equal to Pinot's double accumulation while partial sums stay below 2^53. 1: Pinot's
+ * literal arithmetic, the values added into a double in doc order (AggregationOperator: innerSum per
+ * block of <= 10000 docs, then holder = innerSum + holder, SumAggregationFunction.java:80-92,179-188;
+ * GROUP BY: holder + value per doc, :190-200). Tests bound the difference between the two. */
+static int g_literal_int_sum = 0;
+void oracle_set_literal_int_sum(int32_t on) { g_literal_int_sum = on != 0; }
+int32_t oracle_literal_int_sum(void) { return g_literal_int_sum; }
+static int exact_int_sum(const oracle_column* cols, const oracle_agg* a) {
+  return !g_literal_int_sum && agg_is_int(cols, a);
+}
+
 #define MAX_DOC_PER_CALL 10000 /* pinot-core/.../plan/DocIdSetPlanNode.java:28 */
 
 /* AggregationOperator over blocks of <= 10000 matching docs
@@ -512,7 +524,7 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
           li[a] += len;
           break;
         case OR_AGG_SUM: {
-          if (agg_is_int(cols, &aggs[a])) {  /* exact, see agg_is_int */
+          if (exact_int_sum(cols, &aggs[a])) {  /* exact, see agg_is_int */
             for (int32_t i = 0; i < len; i++) exact[a] += agg_i128(cols, &aggs[a], block[i]);
             break;
           }
@@ -566,7 +578,7 @@ int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t
       out[a] = (double)li[a];
       out_i64[a] = li[a];
       out_hi64[a] = li[a] < 0 ? -1 : 0;
-    } else if (aggs[a].func == OR_AGG_SUM && agg_is_int(cols, &aggs[a])) {
+    } else if (aggs[a].func == OR_AGG_SUM && exact_int_sum(cols, &aggs[a])) {
       out[a] = (double)exact[a];
       out_i64[a] = (int64_t)(uint64_t)(unsigned __int128)exact[a];
       out_hi64[a] = (int64_t)(exact[a] >> 64);
@@ -605,7 +617,7 @@ static void holder_add(or_holder* h, const oracle_column* cols, const oracle_agg
   switch (a->func) {
     case OR_AGG_COUNT: h->li += 1; break;
     case OR_AGG_SUM:
-      if (agg_is_int(cols, a)) h->exact += agg_i128(cols, a, doc);
+      if (exact_int_sum(cols, a)) h->exact += agg_i128(cols, a, doc);
       else h->h = h->h + agg_f64(cols, a, doc);
       break;
     case OR_AGG_SUMLONG: h->li = (int64_t)((uint64_t)h->li + (uint64_t)value_i64(c, doc)); break;
@@ -628,7 +640,7 @@ static void holder_out(const or_holder* h, const oracle_column* cols, const orac
     case OR_AGG_COUNT:
     case OR_AGG_SUMLONG: *out = (double)h->li; *out_i = h->li; *out_hi = h->li < 0 ? -1 : 0; break;
     case OR_AGG_SUM:
-      if (agg_is_int(cols, a)) {
+      if (exact_int_sum(cols, a)) {
         *out = (double)h->exact;
         *out_i = (int64_t)(uint64_t)(unsigned __int128)h->exact;
         *out_hi = (int64_t)(h->exact >> 64);

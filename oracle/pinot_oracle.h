@@ -96,6 +96,9 @@ int64_t oracle_filter(const oracle_column* cols, int64_t num_docs, const oracle_
 int64_t oracle_bitset_to_doc_ids(const uint64_t* bitset, int64_t num_docs, int32_t* out);
 
 /* ---- aggregation (AggregationOperator) ---- */
+/* 1: integer SUMs accumulate in double in doc order as the reference does; 0 (default): exact 128-bit */
+void oracle_set_literal_int_sum(int32_t on);
+int32_t oracle_literal_int_sum(void);
 /* out: per agg one double (COUNT as double too); out_i64 / out_hi64: COUNT / SUMLONG as int64, and an
  * integer SUM's exact 128-bit value as (low, high) words */
 int oracle_aggregate(const oracle_column* cols, int64_t num_docs, const uint64_t* bitset, const oracle_agg* aggs,

@@ -79,3 +79,29 @@ def ssb_flat_segment(name="lineorder_flat_0", split=None):
             cols[c] = (v, t, {"dictionary": dict_enc, "detect_sorted": False})
         segs.append(build_segment(f"{name}_{i}", cols))
     return segs
+
+
+def legacy_inverted_segment(fmt="v1"):
+    """legacyRawInverted with its Pinot-written bitmaps in play: the legacy raw-value inverted index file
+    (RawValueBitmapInvertedIndexCreator) embeds a standard BitmapInvertedIndexWriter section after a
+    44-byte header (LegacyRawValueInvertedIndexCleanup.java:104-114: version 1, cardinality, max length,
+    then dict offset/length and inverted-index offset/length as big-endian longs at bytes 12/20/28/36)
+    whose bitmaps are keyed by the embedded dictionary's order, the sorted distinct values. The
+    category column is rebuilt dictionary-encoded (the decoded strings, sorted dictionary) and gets that
+    embedded section as its inverted index, so EQ/IN predicates expand Pinot-written RoaringBitmaps.
+    The V1 file holds the inverted index; the V3 fixture shares its bytes (same segment)."""
+    import struct
+    import oracle
+    from pinot_amd import segment as S
+    d = os.path.join(GOLDEN, "pinot_written", f"legacyRawInverted_{fmt}")
+    seg = S.load_segment_dir(d)
+    raw = open(os.path.join(GOLDEN, "pinot_written", "legacyRawInverted_v1", "category.bitmap.inv"), "rb").read()
+    version, card, _ = struct.unpack(">iii", raw[:12])
+    _, _, inv_off, inv_len = struct.unpack(">qqqq", raw[12:44])
+    assert version == 1 and inv_off + inv_len == len(raw)
+    vals = np.array(oracle.var_byte_values(seg.columns["category"]), dtype=object)
+    cb = S.build_column("category", vals, S.STRING, dictionary=True)
+    assert cb.cardinality == card
+    cb.inverted = raw[inv_off:inv_off + inv_len]
+    seg.columns["category"] = cb
+    return seg

@@ -114,3 +114,28 @@ def test_raw_string_columns_vs_oracle(engine, version, comp):
         nm, exp = oracle.execute(q, bufs)
         assert res.num_docs_matched() == nm, q
         assert res.groups() == exp, q
+
+
+@pytest.mark.parametrize("fmt", ["v1", "v3"])
+def test_legacy_embedded_bitmaps_on_device(engine, fmt, monkeypatch):
+    """roaring_expand_chunks_kernel over the Pinot-written RoaringBitmaps embedded in the legacy raw-value
+    inverted index (helpers.legacy_inverted_segment): EQ / IN / NOT_EQ counts the reference's
+    LegacyRawValueInvertedIndexMigrationIntegrationTest asserts, and the filter's docIds equal the oracle's."""
+    from helpers import legacy_inverted_segment
+    monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
+    e = EXP["legacy_raw_string"]
+    bufs = legacy_inverted_segment(fmt)
+    seg = engine.ImmutableSegment(bufs)
+    ex = engine.ServerQueryExecutor()
+    c = e["column"]
+    wheres = {f"{c} = '{v}'": cnt for v, cnt in e["counts"].items()}
+    wheres[f"{c} IN ('alpha', 'beta')"] = e["in_alpha_beta"]
+    wheres[f"{c} != 'alpha'"] = e["not_eq_alpha"]
+    for w, cnt in wheres.items():
+        q = f"SELECT COUNT(*) FROM t WHERE {w}"
+        res = ex.execute(q, [seg])
+        assert res.groups()[()][0] == cnt, w
+        ids = ex.filter_doc_ids(q, [seg])[0]
+        bits, _ = oracle.OracleSegment(bufs).filter_bitset(oracle.parse_sql(q), use_inverted=True)
+        exp = np.flatnonzero(np.unpackbits(bits.view(np.uint8), bitorder="little")[:bufs.num_docs])
+        assert np.array_equal(ids, exp), w

@@ -89,3 +89,25 @@ def test_var_byte_writer_reader_round_trip(version, comp):
     cb = S.build_column("c", np.array(vals, dtype=object), S.STRING, dictionary=False, raw_version=version,
                         compression=comp)
     assert oracle.var_byte_values(cb) == vals
+
+
+@pytest.mark.parametrize("fmt", ["v1", "v3"])
+def test_legacy_embedded_bitmaps_through_oracle(fmt):
+    """The Pinot-written RoaringBitmaps embedded in the legacy raw-value inverted index
+    (LegacyRawValueInvertedIndexCleanup.java:104-114) serve EQ / IN / NOT_EQ: the counts
+    LegacyRawValueInvertedIndexMigrationIntegrationTest asserts, and the same docIds as the forward index."""
+    from helpers import legacy_inverted_segment
+    from pinot_amd.query import parse_sql
+    e = EXP["legacy_raw_string"]
+    seg = legacy_inverted_segment(fmt)
+    c = e["column"]
+    wheres = {f"{c} = '{v}'": cnt for v, cnt in e["counts"].items()}
+    wheres[f"{c} IN ('alpha', 'beta')"] = e["in_alpha_beta"]
+    wheres[f"{c} != 'alpha'"] = e["not_eq_alpha"]
+    os_ = oracle.OracleSegment(seg)
+    for w, cnt in wheres.items():
+        q = f"SELECT COUNT(*) FROM t WHERE {w}"
+        assert oracle.execute(q, [seg], use_inverted=True)[0] == cnt, w
+        b_inv, _ = os_.filter_bitset(parse_sql(q), use_inverted=True)
+        b_fwd, _ = os_.filter_bitset(parse_sql(q), use_inverted=False)
+        assert np.array_equal(b_inv, b_fwd), w
