@@ -258,8 +258,22 @@ const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t 
  * exact 128-bit integer sum. EUNSUPPORTED for hash-table plans (merge those by value). */
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops);
-/* Which scan kernel the plan runs: "jit" (query-specialised, compiled with hipRTC) or
- * "aot: <reason>" (the generic precompiled kernel). */
+/* Cross-GPU merge by value (replaces the broker's GroupByDataTableReducer merge of server DataTables,
+ * pinot-core/.../query/reduce/GroupByDataTableReducer.java:258, and IndexedTable.upsert's
+ * AggregationFunction.merge): for GROUP BY results of any plan (dense, partitioned, hash, trimmed).
+ * export_groups writes the result's groups to device memory: h_key_words 64-bit words per group (the
+ * merged key space's ids packed <= 63 bits per word) at d_keys[g * key_words], h_num_acc accumulator
+ * words per group at d_acc[g * num_acc] (the library's encoding). d_keys / d_acc NULL: only the three
+ * sizes. Every rank exports the same layout once the same global key space is installed
+ * (pinot_amd_query_set_group_key_values). merge_groups folds n such rows (every rank's, gathered over
+ * RCCL) into one device hash table with the accumulator ops; until the next execution the result's
+ * groups (num_groups / fetch / fetch_intermediate) are the merged ones. */
+int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64_t* d_acc, int64_t cap,
+                                   int32_t* h_key_words, int32_t* h_num_acc, int64_t* h_num_groups, void* stream);
+int pinot_amd_result_merge_groups(pinot_amd_result* r, const uint64_t* d_keys, const uint64_t* d_acc, int64_t n,
+                                  void* stream);
+/* The device plan: "jit" (fused scan), "jit-select" / "jit-wselect" (selection vector), "jit-partitioned",
+ * "jit-hash", "jit-hash-trim"; " xN" when the batch ran as N shape launches. */
 const char* pinot_amd_result_kernel_info(pinot_amd_result* r);
 /* Algorithmic HBM bytes of the last execution (the roofline numerator): every decoded column once
  * (fixed-bit columns at their bit width, raw columns at their value width); under an inverted-index

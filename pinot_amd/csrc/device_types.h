@@ -146,6 +146,15 @@ struct DevHash {
   unsigned long long* overflow;      // docs that found no free slot (the host fails the query if > 0)
 };
 
+// Group keys by value for the cross-rank merge (the broker reduce on the device): group column j's
+// merged id sits in bits [shift[j], shift[j] + bits) of key word word[j] (the hash plan's packing, <= 63
+// bits per word); a dense table's key decomposes as id_j = (key / stride[j]) % size[j] (mixed radix).
+struct DevKeyPack {
+  int32_t ncols, nw;
+  int32_t word[kMaxGroupCols], shift[kMaxGroupCols];
+  int64_t stride[kMaxGroupCols], size[kMaxGroupCols];
+};
+
 // Uniform per-launch plan (kernel argument of the generated scan kernels and the fixed passes).
 struct DevQuery {
   int32_t nsegs;                            // segments of this launch (DevSegment array length)

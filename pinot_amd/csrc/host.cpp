@@ -40,6 +40,12 @@ hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned lon
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
                                 hipStream_t st);
+hipError_t launch_export_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* hkeys, int64_t cap,
+                                const uint64_t* acc, int32_t nacc_out, const DevKeyPack& kp, uint64_t* out_keys,
+                                uint64_t* out_acc, hipStream_t st);
+hipError_t launch_merge_rows(const uint64_t* keys, const uint64_t* acc, int64_t n, int nw, int nacc_in,
+                             unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q,
+                             unsigned long long* overflow, hipStream_t st);
 hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
@@ -106,6 +112,11 @@ struct DevBuf {
     HIP_OK(hipMemset(p, 0, n));
     if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
     return 0;
+  }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
   }
   int alloc(size_t len) {
     n = len;
@@ -1128,6 +1139,12 @@ struct pinot_amd_result {
   DevBuf skeys, sacc;                  // trim scan table (largest batch)
   DevBuf d_bucket_base, t_hist, t_distinct, t_bstar, t_rank, t_bitmap, t_dstar;
   int fd_acc = -1;                     // ACC_FIRST_DOC accumulator index
+  // cross-rank merge by value (pinot_amd_result_merge_groups): until the next execution the result's
+  // groups are those of the merged table (keys packed as the hash plan packs them)
+  bool merged = false;
+  DevBuf mkeys, macc, movf;
+  int64_t mcap = 0;
+  int mnw = 0;
   // result compaction cache (valid until the next execution)
   bool compacted = false;
   int64_t ngroups = 0;
@@ -1645,6 +1662,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
 }
 
 static int run_plan(pinot_amd_result* r) {
+  r->merged = false;
   hipStream_t st = r->stream;
   r->compacted = false;
   HIP_OK(hipEventRecord(r->ev0, st));
@@ -2874,10 +2892,9 @@ int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms) {
 
 // Compact the non-empty groups on the device (presence bitset -> ballot / prefix-sum compaction ->
 // gather) and copy only those rows to the host; hash-table groups are then put in key order.
-static int compact_groups(pinot_amd_result* r) {
-  if (r->compacted) return 0;
+// the execution's overflow counters: a full hash table or selection vector fails the result
+static int check_overflow(pinot_amd_result* r) {
   hipStream_t st = r->stream;
-  const int nacc = std::max(r->q.nacc, 1);
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
   if (c[3 * r->launches.size() + 1] != 0)
@@ -2891,6 +2908,46 @@ static int compact_groups(pinot_amd_result* r) {
       if (sc[2 * li + 1] != 0)
         return fail(PINOT_AMD_EOVERFLOW, "selection vector of launch %zu overflowed (%llu runs dropped)", li, sc[2 * li + 1]);
   }
+  return 0;
+}
+
+// the group table of the result: the plan's (dense or hash) or, after a cross-rank merge, the merged one
+struct GroupTable {
+  bool hash;
+  int64_t slots;
+  int nwk;
+  const unsigned long long* keys;  // hash tables: nwk x slots key words
+  const uint64_t* acc;
+};
+static GroupTable group_table(const pinot_amd_result* r) {
+  if (r->merged) return {true, r->mcap, r->mnw, (const unsigned long long*)r->mkeys.p, (const uint64_t*)r->macc.p};
+  if (r->kind == PLAN_HASH) return {true, r->fcap, r->nw, (const unsigned long long*)r->fkeys.p, (const uint64_t*)r->acc.p};
+  return {false, r->q.num_keys, 1, nullptr, (const uint64_t*)r->acc.p};
+}
+
+// device compaction of a group table's non-empty slots (COUNT != 0), ascending: slot indices in idx
+static int compact_slots(const GroupTable& T, hipStream_t st, DevBuf& idx, int64_t* ng) {
+  DevBuf bits, counts, total;
+  if (int rc = bits.alloc((size_t)((T.slots + 63) / 64 + 1) * 8)) return rc;
+  HIP_OK(launch_presence_bitset(T.acc, T.slots, (unsigned long long*)bits.p, st));
+  const int64_t nc = compact_num_chunks(T.slots);
+  if (int rc = counts.alloc((size_t)nc * 8)) return rc;
+  if (int rc = total.alloc(8)) return rc;
+  HIP_OK(launch_bitset_count((const uint64_t*)bits.p, T.slots, (int64_t*)counts.p, (int64_t*)total.p, st));
+  HIP_OK(hipMemcpyAsync(ng, total.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (*ng > 0) {
+    if (int rc = idx.alloc((size_t)*ng * 4)) return rc;
+    HIP_OK(launch_bitset_compact((const uint64_t*)bits.p, T.slots, (const int64_t*)counts.p, (int32_t*)idx.p, st));
+  }
+  return 0;
+}
+
+static int compact_groups(pinot_amd_result* r) {
+  if (r->compacted) return 0;
+  hipStream_t st = r->stream;
+  const int nacc = std::max(r->q.nacc, 1);
+  if (int rc = check_overflow(r)) return rc;
   if (r->num_group_by == 0 || r->q.nacc == 0) {
     r->ngroups = 1;
     r->ckeys.assign(1, 0);
@@ -2902,29 +2959,20 @@ static int compact_groups(pinot_amd_result* r) {
     r->compacted = true;
     return 0;
   }
-  const bool hash = r->kind == PLAN_HASH;
-  const int64_t slots = hash ? r->fcap : r->q.num_keys;
-  const int nwk = hash ? r->nw : 1;
-  DevBuf bits, counts, total, idx, okeys, oacc;
-  if (int rc = bits.alloc((size_t)((slots + 63) / 64 + 1) * 8)) return rc;
-  HIP_OK(launch_presence_bitset((const uint64_t*)r->acc.p, slots, (unsigned long long*)bits.p, st));
-  const int64_t nc = compact_num_chunks(slots);
-  if (int rc = counts.alloc((size_t)nc * 8)) return rc;
-  if (int rc = total.alloc(8)) return rc;
-  HIP_OK(launch_bitset_count((const uint64_t*)bits.p, slots, (int64_t*)counts.p, (int64_t*)total.p, st));
+  const GroupTable T = group_table(r);
+  const bool hash = T.hash;
+  const int nwk = T.nwk;
+  DevBuf idx, okeys, oacc;
   int64_t ng = 0;
-  HIP_OK(hipMemcpyAsync(&ng, total.p, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  if (int rc = compact_slots(T, st, idx, &ng)) return rc;
   r->ngroups = ng;
   r->ckeys.assign((size_t)ng * nwk, 0);
   r->cacc.assign((size_t)ng * nacc, 0);
   if (ng > 0) {
-    if (int rc = idx.alloc((size_t)ng * 4)) return rc;
     if (int rc = okeys.alloc((size_t)ng * nwk * 8)) return rc;
     if (int rc = oacc.alloc((size_t)ng * nacc * 8)) return rc;
-    HIP_OK(launch_bitset_compact((const uint64_t*)bits.p, slots, (const int64_t*)counts.p, (int32_t*)idx.p, st));
-    HIP_OK(launch_gather_groups((const int32_t*)idx.p, ng, hash ? (const unsigned long long*)r->fkeys.p : nullptr, nwk,
-                                slots, (const uint64_t*)r->acc.p, nacc, (uint64_t*)okeys.p, (uint64_t*)oacc.p, st));
+    HIP_OK(launch_gather_groups((const int32_t*)idx.p, ng, T.keys, nwk, T.slots, T.acc, nacc, (uint64_t*)okeys.p,
+                                (uint64_t*)oacc.p, st));
     HIP_OK(hipMemcpyAsync(r->ckeys.data(), okeys.p, r->ckeys.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(r->cacc.data(), oacc.p, r->cacc.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -2993,8 +3041,8 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
   if (int rc = no_throw("fetch", [&] { return compact_groups(r); })) return rc;
   const int na = (int)r->agg_type.size();
   const int nacc = std::max(r->q.nacc, 1);
-  const bool hash = r->kind == PLAN_HASH;
-  const int nwk = hash ? r->nw : 1;
+  const bool hash = r->kind == PLAN_HASH || r->merged;
+  const int nwk = r->merged ? r->mnw : hash ? r->nw : 1;
   if (r->ngroups > cap) return fail(PINOT_AMD_EOVERFLOW, "fetch: %lld groups exceed capacity %lld", (long long)r->ngroups,
                                     (long long)cap);
   for (int64_t g = 0; g < r->ngroups; ++g) {
@@ -3116,8 +3164,9 @@ const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t 
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops) {
   if (!r || !h_num_slots || !h_num_key_slots) return fail(PINOT_AMD_EINVAL, "accumulators: bad arguments");
-  if (r->kind == PLAN_HASH)
-    return fail(PINOT_AMD_EUNSUPPORTED, "accumulators: hash-table results merge by value (pinot_amd_result_fetch)");
+  if (r->kind == PLAN_HASH || r->merged)
+    return fail(PINOT_AMD_EUNSUPPORTED, "accumulators: hash-table (and merged) results merge by value "
+                                        "(pinot_amd_result_export_groups / pinot_amd_result_merge_groups)");
   *h_num_slots = r->q.nacc;
   *h_num_key_slots = r->q.num_keys;
   for (int a = 0; a < r->q.nacc; ++a) {
@@ -3137,3 +3186,102 @@ int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Cross-rank merge by value (the broker reduce, GroupByDataTableReducer.java:258, on the device)
+// ------------------------------------------------------------------------------------------------
+// The hash plan's key packing over the result's merged key space (identical on every rank once the
+// global key space is installed), and the dense table's mixed-radix strides.
+static int key_pack(const pinot_amd_result* r, DevKeyPack* kp) {
+  memset(kp, 0, sizeof(*kp));
+  kp->ncols = r->num_group_by;
+  if (kp->ncols > kMaxGroupCols) return fail(PINOT_AMD_EUNSUPPORTED, "export: %d group columns", kp->ncols);
+  int w = 0, sh = 0;
+  for (int j = 0; j < kp->ncols; ++j) {
+    const int64_t size = (int64_t)std::max<size_t>(r->keys[j].size(), 1);
+    const int b = bits_for(size);
+    if (sh + b > 63) { ++w; sh = 0; }
+    kp->word[j] = w;
+    kp->shift[j] = sh;
+    kp->size[j] = size;
+    kp->stride[j] = j < (int)r->key_stride.size() ? std::max<int64_t>(r->key_stride[j], 1) : 1;
+    sh += b;
+  }
+  kp->nw = w + 1;
+  if (kp->nw > kMaxKeyWords) return fail(PINOT_AMD_EUNSUPPORTED, "group key of %d words exceeds %d", kp->nw, kMaxKeyWords);
+  return 0;
+}
+
+// accumulators exported per group: every array but the trimming plans' first-docId (always last)
+static int export_nacc(const pinot_amd_result* r) { return r->fd_acc >= 0 ? r->fd_acc : r->q.nacc; }
+
+int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64_t* d_acc, int64_t cap,
+                                   int32_t* h_key_words, int32_t* h_num_acc, int64_t* h_num_groups, void* stream) {
+  if (!r || !h_key_words || !h_num_acc || !h_num_groups || cap < 0)
+    return fail(PINOT_AMD_EINVAL, "export_groups: bad arguments");
+  return no_throw("export_groups", [&]() -> int {
+    if (r->num_group_by == 0 || r->q.nacc == 0)
+      return fail(PINOT_AMD_EUNSUPPORTED, "export_groups: not a GROUP BY result with aggregations");
+    if (r->merged) return fail(PINOT_AMD_EINVAL, "export_groups: result already merged");
+    if (stream) r->stream = (hipStream_t)stream;
+    DevKeyPack kp;
+    if (int rc = key_pack(r, &kp)) return rc;
+    if (r->kind == PLAN_HASH && kp.nw != r->nw) return fail(PINOT_AMD_EINVAL, "export_groups: key packing mismatch");
+    if (int rc = check_overflow(r)) return rc;
+    const GroupTable T = group_table(r);
+    DevBuf idx;
+    int64_t ng = 0;
+    if (int rc = compact_slots(T, r->stream, idx, &ng)) return rc;
+    *h_key_words = kp.nw;
+    *h_num_acc = export_nacc(r);
+    *h_num_groups = ng;
+    if (!d_keys || !d_acc) return 0;  // sizing call
+    if (ng > cap) return fail(PINOT_AMD_EOVERFLOW, "export_groups: %lld groups exceed capacity %lld", (long long)ng,
+                              (long long)cap);
+    HIP_OK(launch_export_groups((const int32_t*)idx.p, ng, T.keys, T.slots, T.acc, export_nacc(r), kp, d_keys, d_acc,
+                                r->stream));
+    HIP_OK(hipStreamSynchronize(r->stream));
+    return 0;
+  });
+}
+
+int pinot_amd_result_merge_groups(pinot_amd_result* r, const uint64_t* d_keys, const uint64_t* d_acc, int64_t n,
+                                  void* stream) {
+  if (!r || n < 0 || (n > 0 && (!d_keys || !d_acc))) return fail(PINOT_AMD_EINVAL, "merge_groups: bad arguments");
+  return no_throw("merge_groups", [&]() -> int {
+    if (r->num_group_by == 0 || r->q.nacc == 0)
+      return fail(PINOT_AMD_EUNSUPPORTED, "merge_groups: not a GROUP BY result with aggregations");
+    if (stream) r->stream = (hipStream_t)stream;
+    hipStream_t st = r->stream;
+    DevKeyPack kp;
+    if (int rc = key_pack(r, &kp)) return rc;
+    r->merged = false;
+    r->mcap = next_pow2(std::max<int64_t>(64, 2 * n));
+    if (r->mcap > ((int64_t)1 << 31)) return fail(PINOT_AMD_EUNSUPPORTED, "merge_groups: %lld rows", (long long)n);
+    r->mnw = kp.nw;
+    r->mkeys.reset();
+    r->macc.reset();
+    r->movf.reset();
+    if (int rc = r->mkeys.alloc((size_t)r->mcap * kp.nw * 8)) return rc;
+    if (int rc = r->macc.alloc((size_t)r->mcap * r->q.nacc * 8)) return rc;
+    if (int rc = r->movf.alloc(8)) return rc;
+    HIP_OK(hipMemsetAsync(r->mkeys.p, 0xFF, r->mkeys.n, st));
+    HIP_OK(hipMemsetAsync(r->movf.p, 0, 8, st));
+    HIP_OK(launch_init_acc((uint64_t*)r->macc.p, r->q, r->mcap, st));
+    HIP_OK(launch_merge_rows(d_keys, d_acc, n, kp.nw, export_nacc(r), (unsigned long long*)r->mkeys.p, r->mcap,
+                             (uint64_t*)r->macc.p, r->q, (unsigned long long*)r->movf.p, st));
+    unsigned long long ovf = 0;
+    HIP_OK(hipMemcpyAsync(&ovf, r->movf.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (ovf) return fail(PINOT_AMD_EOVERFLOW, "merge_groups: %llu rows without a slot", ovf);
+    if (r->kind != PLAN_HASH) {  // fetch decodes merged keys with the hash plan's packing
+      r->pack_word.assign(kp.word, kp.word + kp.ncols);
+      r->pack_shift.assign(kp.shift, kp.shift + kp.ncols);
+      r->pack_bits.clear();
+      for (int j = 0; j < kp.ncols; ++j) r->pack_bits.push_back(bits_for(kp.size[j]));
+    }
+    r->merged = true;
+    r->compacted = false;
+    return 0;
+  });
+}

@@ -281,6 +281,50 @@ __global__ void gather_groups_kernel(const int32_t* slots, int64_t ngroups, cons
   }
 }
 
+// Cross-rank merge by value (GroupByDataTableReducer's merge of every server's groups, here every
+// GPU's): each rank exports its compacted groups as (packed key words, accumulator words), the ranks
+// all-gather them over RCCL, and every rank folds all rows into one hash table with the accumulator
+// ops (AggregationFunction.merge) -- whatever plan (dense, partitioned, hash, trimmed) each rank ran.
+__global__ void export_groups_kernel(const int32_t* slots, int64_t ngroups, const unsigned long long* hkeys,
+                                     int64_t cap, const uint64_t* acc, int32_t nacc_out, DevKeyPack kp,
+                                     uint64_t* out_keys, uint64_t* out_acc) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t slot = (uint64_t)(uint32_t)slots[g];
+    if (hkeys) {
+      for (int w = 0; w < kp.nw; ++w) out_keys[g * kp.nw + w] = hkeys[(uint64_t)w * (uint64_t)cap + slot];
+    } else {
+      uint64_t kw[kMaxKeyWords];
+      for (int w = 0; w < kp.nw; ++w) kw[w] = 0ull;
+      for (int j = 0; j < kp.ncols; ++j) {
+        const uint64_t id = (slot / (uint64_t)kp.stride[j]) % (uint64_t)kp.size[j];
+        kw[kp.word[j]] |= id << kp.shift[j];
+      }
+      for (int w = 0; w < kp.nw; ++w) out_keys[g * kp.nw + w] = kw[w];
+    }
+    for (int a = 0; a < nacc_out; ++a) out_acc[g * nacc_out + a] = acc[(uint64_t)a * (uint64_t)cap + slot];
+  }
+}
+
+__global__ void merge_rows_kernel(const uint64_t* keys, const uint64_t* acc, int64_t n, int nw, int nacc_in,
+                                  unsigned long long* fkeys, int64_t fcap, uint64_t* facc, DevQuery q,
+                                  unsigned long long* overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t kw[kMaxKeyWords];
+    for (int w = 0; w < nw; ++w) kw[w] = keys[i * nw + w];
+    const int64_t slot = hash_find_rt(fkeys, fcap, nw, kw);
+    if (slot < 0) {
+      atomicAdd(overflow, 1ull);
+      continue;
+    }
+    for (int a = 0; a < nacc_in; ++a) {
+      const uint64_t v = acc[i * nacc_in + a];
+      const uint64_t vh = a + 1 < nacc_in ? acc[i * nacc_in + a + 1] : 0ull;
+      acc_apply(q.acc_op[a], facc + (uint64_t)a * (uint64_t)fcap + slot,
+                facc + (uint64_t)(a + 1 < nacc_in ? a + 1 : a) * (uint64_t)fcap + slot, v, vh);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Low-level operators
 // ------------------------------------------------------------------------------------------------
@@ -994,6 +1038,24 @@ hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const uns
   if (ngroups <= 0) return hipSuccess;
   hipLaunchKernelGGL(gather_groups_kernel, dim3(grid_cap(ngroups, kBlock, 8192)), dim3(kBlock), 0, st, slots, ngroups,
                      keys, nw, cap, acc, nacc, out_keys, out_acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_export_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* hkeys, int64_t cap,
+                                const uint64_t* acc, int32_t nacc_out, const DevKeyPack& kp, uint64_t* out_keys,
+                                uint64_t* out_acc, hipStream_t st) {
+  if (ngroups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(export_groups_kernel, dim3(grid_cap(ngroups, kBlock, 8192)), dim3(kBlock), 0, st, slots, ngroups,
+                     hkeys, cap, acc, nacc_out, kp, out_keys, out_acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_rows(const uint64_t* keys, const uint64_t* acc, int64_t n, int nw, int nacc_in,
+                             unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q,
+                             unsigned long long* overflow, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_rows_kernel, dim3(grid_cap(n, kBlock, 8192)), dim3(kBlock), 0, st, keys, acc, n, nw, nacc_in,
+                     fkeys, fcap, facc, q, overflow);
   return hipGetLastError();
 }
 

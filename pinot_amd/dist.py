@@ -6,12 +6,14 @@ accumulator table over the query's merged key space (accumulation across its own
 in-kernel), and the tables of all GPUs are merged in place with RCCL all-reduces over xGMI:
 SUM/COUNT as int64 or fp64 sums, MIN/MAX as min/max of an order-preserving int64 encoding of the
 double value. Small tables go through one all-gather reduced locally; no other data-path collective.
+Results without a shared dense table (hash-table plans, numGroupsLimit trimming, DISTINCTCOUNT) merge
+by value on the device: one all-gather of every rank's compacted (key words, accumulator words) rows,
+folded into one device hash table by the library.
 
 Every rank plans the query over the same group key space: ``global_key_space`` all-gathers each
 rank's group-by column values and the union is installed on every rank
 (``pinot_amd_query_set_group_key_values``), so dense tables index identical groups whatever each
-rank's own dictionaries hold. Results without a dense table (hash-table GROUP BY, DISTINCTCOUNT)
-merge by value like the broker (``merge_groups``).
+rank's own dictionaries hold, and the by-value rows of every rank pack their keys identically.
 """
 from __future__ import annotations
 
@@ -148,24 +150,77 @@ class _DeviceWords:
 
 
 def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes: int = 1 << 20):
-    """Merge a QueryResult's dense accumulators across ranks, in place in the library's HBM table (a
-    zero-copy torch view of it; rows are contiguous in one allocation). The result must have been
-    executed on torch's current stream (or that stream synchronised). Every rank must have run the
-    query over the same key space (global_key_space). `scratch` is unused (kept for callers)."""
+    """Merge a query result across ranks; afterwards every rank's result holds the merged groups.
+
+    The ranks first agree on HOW (one all-reduce of a flag): when every rank's result keeps its groups in
+    a dense accumulator table (identical key space via global_key_space) the tables are merged in place
+    (merge_tables on a zero-copy torch view of the library's HBM table); when any rank ran a hash-table
+    plan (large key spaces, numGroupsLimit trimming) or the query has DISTINCTCOUNT, every rank merges BY
+    VALUE on the device: export_groups -> one all-gather of the (key words, accumulator words) rows ->
+    merge_groups folds all ranks' rows into one device hash table (GroupByDataTableReducer's merge). A
+    rank never decides alone, so ranks whose plans differ still run the same collectives.
+
+    `stream`: the stream the result was executed on; torch's current stream waits for it first.
+    `scratch` is unused (kept for callers)."""
     import torch
-    ops, nk, ptrs = result.accumulators()
-    if not ops:
+    import torch.distributed as dist
+    cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+    if stream is not None and cur is not None:
+        handle = int(getattr(stream, "cuda_stream", stream))
+        if handle != cur.cuda_stream:
+            ext = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(handle)
+            cur.wait_stream(ext)
+    parts = result.results() if hasattr(result, "results") else [result]
+    world = dist.get_world_size(group)
+    if world == 1:
         return scratch
-    table = torch.as_tensor(_DeviceWords(ptrs[0], len(ops) * nk), device="cuda")
-    assert table.data_ptr() == ptrs[0], "zero-copy view of the accumulator table failed"
-    merge_tables(table, ops, nk, group, gather_max_bytes)
+    # DISTINCTCOUNT folds (group key, value) groups whose value column is not in the dense key space
+    local_by_value = hasattr(result, "results") or any(not p.has_dense_table() for p in parts)
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    flag = torch.tensor([1 if local_by_value else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        for p in parts:
+            keys, acc = p.export_groups(stream=cur)
+            rows = gather_rows(torch.cat([keys, acc], dim=1), group)
+            kw = keys.shape[1]
+            p.merge_groups(rows[:, :kw].contiguous(), rows[:, kw:].contiguous(), stream=cur)
+        return scratch
+    for p in parts:
+        ops, nk, ptrs = p.accumulators()
+        if not ops:
+            continue
+        table = torch.as_tensor(_DeviceWords(ptrs[0], len(ops) * nk), device="cuda")
+        assert table.data_ptr() == ptrs[0], "zero-copy view of the accumulator table failed"
+        merge_tables(table, ops, nk, group, gather_max_bytes)
     return scratch
 
 
+def gather_rows(rows, group=None):
+    """All-gather every rank's [n_r, w] int64 rows (n_r may differ) into the concatenation in rank order:
+    one all-gather of the row counts, one of the rows padded to the largest count."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    counts = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts)
+    w = rows.shape[1]
+    if m == 0:
+        return rows.new_empty((0, w))
+    buf = rows.new_zeros((m, w))
+    buf[:rows.shape[0]] = rows
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)]).contiguous()
+
+
 def merge_groups(qc, groups: dict, group=None) -> dict:
-    """Broker-style merge by value (GroupByDataTableReducer.java:258 / AggregationFunction.merge) of
-    every rank's fetched groups: for results without a shared dense table (hash-table GROUP BY,
-    DISTINCTCOUNT sets). Returns the merged groups on every rank."""
+    """Host merge by value of every rank's fetched groups (GroupByDataTableReducer.java:258 /
+    AggregationFunction.merge) through all_gather_object: the reference semantics merge_result's device
+    path implements, kept for callers holding groups() dicts (small results, tests)."""
     import torch.distributed as dist
     from .query import merge_partial
     world = dist.get_world_size(group)
@@ -199,6 +254,16 @@ def local_key_values(segments, column: str, executor=None) -> list:
             vals.setdefault(distinct_value(v), v)
         res.destroy()
     return list(vals.values())
+
+
+def key_columns(qc) -> list:
+    """Columns whose key space must be global for a cross-rank merge: the GROUP BY columns, and the
+    DISTINCTCOUNT columns (their device queries group by them too)."""
+    cols = list(qc.group_by)
+    for a in qc.aggregations:
+        if a.func == "DISTINCTCOUNT" and a.column not in cols:
+            cols.append(a.column)
+    return cols
 
 
 def global_key_space(segments, group_by: Sequence[str], group=None, executor=None) -> dict:

@@ -191,8 +191,14 @@ class DistinctCountResult:
         return sum(r.algorithmic_bytes() for r in self._all())
 
     def accumulators(self):
-        raise NotImplementedError("DISTINCTCOUNT results merge as value sets (groups()), not as accumulator "
-                                  "tables: the cross-GPU merge of dist.merge_result is single-rank only for them")
+        raise NotImplementedError("DISTINCTCOUNT results merge by value (dist.merge_result merges each of "
+                                  "results() with export_groups / merge_groups), not as one accumulator table")
+
+    def results(self):
+        """The device results this one folds: the base query, then one per DISTINCTCOUNT (each a GROUP BY
+        whose groups are (group key, distinct value) pairs: merged by value across ranks, they union the
+        value sets)."""
+        return self._all()
 
     def destroy(self) -> None:
         for r in self._all():
@@ -248,6 +254,38 @@ class QueryResult:
         ops = (C.c_int32 * n.value)()
         check(lib().pinot_amd_result_accumulators(self._h, C.byref(n), C.byref(nk), ptrs, ops), "accumulators")
         return list(ops), nk.value, [int(p) for p in ptrs]
+
+    def has_dense_table(self) -> bool:
+        """True when the groups live in a dense accumulator table over the key space (mergeable in place
+        across ranks with all-reduces); False for hash-table plans and merged results."""
+        n = C.c_int32()
+        nk = C.c_int64()
+        return lib().pinot_amd_result_accumulators(self._h, C.byref(n), C.byref(nk), None, None) == 0
+
+    def export_groups(self, stream=None):
+        """This result's groups as device tensors for a cross-rank merge by value
+        (pinot_amd_result_export_groups): keys [groups, key_words] and accumulator words [groups, num_acc],
+        int64, written on `stream` (synchronised before returning)."""
+        import torch
+        L = lib()
+        kw, na, ng = C.c_int32(), C.c_int32(), C.c_int64()
+        sh = _stream_handle(stream)
+        check(L.pinot_amd_result_export_groups(self._h, None, None, 0, C.byref(kw), C.byref(na), C.byref(ng), sh),
+              "export_groups")
+        keys = torch.empty((ng.value, kw.value), dtype=torch.int64, device="cuda")
+        acc = torch.empty((ng.value, na.value), dtype=torch.int64, device="cuda")
+        if ng.value:
+            torch.cuda.current_stream().synchronize()  # the allocations are ordered on torch's stream
+            check(L.pinot_amd_result_export_groups(self._h, keys.data_ptr(), acc.data_ptr(), ng.value, C.byref(kw),
+                                                   C.byref(na), C.byref(ng), sh), "export_groups")
+        return keys, acc
+
+    def merge_groups(self, keys, acc, stream=None) -> None:
+        """Fold gathered (keys, acc) rows of every rank into this result (pinot_amd_result_merge_groups):
+        until the next execution, groups() are the merged groups. The tensors must be ready on `stream`."""
+        assert keys.is_contiguous() and acc.is_contiguous() and keys.shape[0] == acc.shape[0]
+        check(lib().pinot_amd_result_merge_groups(self._h, keys.data_ptr(), acc.data_ptr(), keys.shape[0],
+                                                  _stream_handle(stream)), "merge_groups")
 
     def groups(self) -> Dict[tuple, list]:
         """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation."""
