@@ -170,6 +170,16 @@ struct DevQuery {
   int64_t sel_cap;
   int32_t sel_chunk;     // vector entries a select wave reserves at a time (planner: from the expected matches)
   int32_t sel_pad;
+  // numGroupsLimit admission of dense trimming plans (JitPlan::admit / firstdoc): bit `key` of segment
+  // key_seg's bitmap (admit_words 32-bit words per segment) = the segment admitted that group. The
+  // first-doc pass keeps first[key_seg * num_keys + key] = the key's smallest matching docId so far and
+  // appends each key it sees first to that segment's list (seen[key_seg * seen_cap ..], count seen_n[key_seg])
+  const uint32_t* admit;
+  int64_t admit_words;
+  uint32_t* first;
+  uint32_t* seen;
+  unsigned long long* seen_n;
+  int64_t seen_cap;
 };
 
 }  // namespace pamd

@@ -36,6 +36,10 @@ hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, 
 hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int nw, int has_seg, const uint64_t* sacc,
                              unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q, int fd_acc,
                              const int64_t* dstar, unsigned long long* overflow, hipStream_t st);
+hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const unsigned long long* seen_n, int64_t cap,
+                        int32_t nsegs, int64_t limit, const int64_t* bucket_base, int64_t max_buckets, uint32_t* hist,
+                        int64_t* bstar, int64_t* rank, unsigned long long* bitmap, int64_t* dstar,
+                        unsigned long long* limit_reached, int phase, uint32_t* admit, int64_t words, hipStream_t st);
 hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st);
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
@@ -1079,6 +1083,12 @@ struct Launch {
   int rec_bytes = 0;
   bool part_sampled = false;
   int64_t region_cap = 0;  // records the partition regions can hold
+  // dense numGroupsLimit admission: the first-doc pass over each segment's prefix (d_fd_segs: the
+  // launch's segments cut to their prefixes), or over whole segments (d_segs) when a prefix saw too few keys
+  JitKernel* jit_fd = nullptr;
+  DevBuf d_fd_segs;
+  DevQuery fd_q{};
+  int fd_grid = 1, fd_full_grid = 1;
 };
 
 enum PlanKind { PLAN_DENSE = 0, PLAN_PARTITIONED = 1, PLAN_HASH = 2, PLAN_FILTER = 3 };
@@ -1139,6 +1149,13 @@ struct pinot_amd_result {
   DevBuf skeys, sacc;                  // trim scan table (largest batch)
   DevBuf d_bucket_base, t_hist, t_distinct, t_bstar, t_rank, t_bitmap, t_dstar;
   int fd_acc = -1;                     // ACC_FIRST_DOC accumulator index
+  // dense numGroupsLimit admission (trimming over a key space a dense table holds): per segment the first
+  // matching docId of every key seen in its prefix, the list of those keys, and the admission bitmaps
+  bool admit = false;
+  DevBuf a_first, a_seen, a_seen_n, a_bits, a_hist, a_bbase, a_bstar, a_rank, a_bitmap, a_dstar;
+  int64_t a_cap = 0, a_words = 0, a_buckets = 0, a_max_buckets = 0;
+  std::vector<int64_t> a_prefix;       // docs of each segment the first pass reads
+  std::vector<int64_t> a_docs;
   // cross-rank merge by value (pinot_amd_result_merge_groups): until the next execution the result's
   // groups are those of the merged table (keys packed as the hash plan packs them)
   bool merged = false;
@@ -1661,6 +1678,61 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   return 0;
 }
 
+// Dense numGroupsLimit admission, every execution: the first-doc pass over each segment's prefix, the
+// limit-th first docId per segment, the admission bitmaps. A segment whose prefix saw fewer than
+// numGroupsLimit keys (though the segment may hold more) is redone over whole segments (one host check).
+static int run_admission(pinot_amd_result* r, unsigned long long* limit_flag) {
+  hipStream_t st = r->stream;
+  const int32_t n = (int32_t)r->a_prefix.size();
+  const int64_t nk = r->q.num_keys;
+  HIP_OK(hipMemsetAsync(r->a_seen_n.p, 0, r->a_seen_n.n, st));
+  auto first_pass = [&](bool full) -> int {
+    for (auto& L : r->launches) {
+      const DevSegment* sg = (const DevSegment*)(full ? L.d_segs.p : L.d_fd_segs.p);
+      DevQuery fq = L.fd_q;
+      if (full) fq.total_tiles = L.q.total_tiles;
+      if (fq.total_tiles == 0) continue;
+      uint64_t* table = nullptr;
+      uint64_t* const* bits = nullptr;
+      unsigned long long* matched = nullptr;
+      DevHash h{};
+      void* args[] = {(void*)&sg, (void*)&fq, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
+      HIP_OK(hipModuleLaunchKernel(L.jit_fd->fn, (unsigned)(full ? L.fd_full_grid : L.fd_grid), 1, 1, kBlock, 1, 1, 0, st,
+                                   args, nullptr));
+    }
+    return 0;
+  };
+  auto select = [&]() -> int {
+    HIP_OK(hipMemsetAsync(r->a_hist.p, 0, r->a_hist.n, st));
+    HIP_OK(launch_admit((uint32_t*)r->a_first.p, nk, (const uint32_t*)r->a_seen.p, (const unsigned long long*)r->a_seen_n.p,
+                        r->a_cap, n, r->limit, (const int64_t*)r->a_bbase.p, r->a_max_buckets, (uint32_t*)r->a_hist.p,
+                        (int64_t*)r->a_bstar.p, (int64_t*)r->a_rank.p, nullptr, nullptr, limit_flag, 0, nullptr, 0, st));
+    return 0;
+  };
+  if (int rc = first_pass(false)) return rc;
+  if (int rc = select()) return rc;
+  std::vector<unsigned long long> seen((size_t)n);
+  HIP_OK(hipMemcpyAsync(seen.data(), r->a_seen_n.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  bool redo = false;
+  for (int32_t si = 0; si < n; ++si) {
+    if (seen[si] > (unsigned long long)r->a_cap) return fail(PINOT_AMD_EOVERFLOW, "admission: key list overflow");
+    redo |= r->a_prefix[si] > 0 && r->a_prefix[si] < r->a_docs[si] && (int64_t)seen[si] < r->limit;
+  }
+  if (redo) {  // keys beyond the prefix matter: the whole segments (atomicMin keeps what the prefix found)
+    HIP_OK(hipMemsetAsync(limit_flag, 0, 8, st));
+    if (int rc = first_pass(true)) return rc;
+    if (int rc = select()) return rc;
+  }
+  HIP_OK(hipMemsetAsync(r->a_bitmap.p, 0, r->a_bitmap.n, st));
+  HIP_OK(hipMemsetAsync(r->a_bits.p, 0, r->a_bits.n, st));
+  HIP_OK(launch_admit((uint32_t*)r->a_first.p, nk, (const uint32_t*)r->a_seen.p, (const unsigned long long*)r->a_seen_n.p,
+                      r->a_cap, n, r->limit, (const int64_t*)r->a_bbase.p, r->a_max_buckets, (uint32_t*)r->a_hist.p,
+                      (int64_t*)r->a_bstar.p, (int64_t*)r->a_rank.p, (unsigned long long*)r->a_bitmap.p,
+                      (int64_t*)r->a_dstar.p, limit_flag, 1, (uint32_t*)r->a_bits.p, r->a_words, st));
+  return 0;
+}
+
 static int run_plan(pinot_amd_result* r) {
   r->merged = false;
   hipStream_t st = r->stream;
@@ -1710,6 +1782,8 @@ static int run_plan(pinot_amd_result* r) {
       }
     }
   } else {
+    if (r->admit)
+      if (int rc = run_admission(r, limit_flag)) return rc;
     if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, r->q.num_keys, st));
     DevHash H{};
     for (size_t li = 0; li < nl; ++li)
@@ -1916,6 +1990,28 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
   r->limit_possible = limit_possible;
+  // admission prefixes (dense trimming): the docs of segment si that should hold numGroupsLimit distinct
+  // keys, twice the coupon-collector expectation for K uniform keys (K ln(K / (K - L)) matching docs,
+  // scaled by the segment's selectivity) plus 64 Ki docs; a segment that cannot reach the limit needs
+  // no pass (everything admitted). A prefix that still sees fewer keys is redone over the whole segment.
+  auto admit_prefixes = [&]() {
+    r->a_prefix.assign(n, 0);
+    r->a_docs.assign(n, 0);
+    for (int si = 0; si < n; ++si) {
+      const int64_t nd = segs[si]->num_docs;
+      r->a_docs[si] = nd;
+      if (seg_bound[si] < Q.num_groups_limit) continue;
+      double ks = 1;
+      for (auto& g : Q.group_by) ks *= (double)std::max(segs[si]->cols.at(g)->card, 1);
+      const double L = (double)Q.num_groups_limit;
+      const double need = ks > L ? ks * std::log(ks / (ks - L)) : (double)nd;
+      const double sel = (!seg_matched.empty() && nd > 0) ? std::max((double)seg_matched[si] / (double)nd, 1e-9) : 1.0;
+      const double rows = 2.0 * need / sel + 65536.0;
+      int64_t pfx = rows >= (double)nd ? nd : ((int64_t)rows + kTileDocs - 1) / kTileDocs * kTileDocs;
+      if (const char* e = getenv("PINOT_AMD_ADMIT_PREFIX")) pfx = std::min<int64_t>(nd, std::max<int64_t>(kTileDocs, atoll(e)));
+      r->a_prefix[si] = std::min(pfx, nd);
+    }
+  };
 
   // ---- accumulators: acc 0 = COUNT; others grouped by slot; ACC_FIRST_DOC last ----
   // nan_skip: MinMaxRangePair.apply compares with < / >, so NaN never enters the pair (MIN / MAX of
@@ -1998,12 +2094,26 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     r->kind = PLAN_FILTER;
   } else if (Q.group_by.empty()) {
     r->kind = PLAN_DENSE;
+  } else if (limit_possible && dense_keys <= (double)dense_cap && !env_is("PINOT_AMD_GROUP_PLAN", "hash") &&
+             !env_is("PINOT_AMD_TRIM_PLAN", "hash") && [&]() {
+               // dense admission: first docIds (4 B per segment and key), key lists, bitmaps within budget;
+               // a segment's 1024-doc bucket histogram within one block's LDS
+               int64_t max_docs = 0;
+               for (auto* sg : segs) max_docs = std::max(max_docs, sg->num_docs);
+               const double cap = std::min((double)max_docs, dense_keys);
+               const double bytes = (double)n * (dense_keys * 4.0 + cap * 4.0 + dense_keys / 8.0);
+               return bytes <= (double)env_i64("PINOT_AMD_ADMIT_MAX_BYTES", (int64_t)8 << 30) &&
+                      (max_docs + 1023) / 1024 * 4 <= 64 * 1024;
+             }()) {
+    r->kind = PLAN_DENSE;
+    r->admit = true;
   } else if (limit_possible || dense_keys > (double)dense_cap || env_is("PINOT_AMD_GROUP_PLAN", "hash")) {
     r->kind = PLAN_HASH;
     r->trim = limit_possible;
   } else {
     r->kind = PLAN_DENSE;
   }
+  if (r->admit) admit_prefixes();
   if (r->trim) {
     r->fd_acc = nacc;
     if (int rc = push_acc({-1, ACC_FIRST_DOC, 0, -1, 0})) return rc;
@@ -2162,6 +2272,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   for (int a = 1; a < q.nacc; ++a)
     base.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2, acc_req[a].nan_skip});
   base.num_keys = num_keys;
+  base.admit = r->admit;
   base.bitset = filter_only;
   base.aggregate = q.nacc > 0;
   int cus = 256;
@@ -2325,7 +2436,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     return c.enc == ENC_FIXED_BIT ? c.bits / 8.0 : c.enc == ENC_RAW ? (double)value_size(c.type) : 0.0;
   };
   const char* sel_env = getenv("PINOT_AMD_SELECT");
-  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !base.partitioned &&
+  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit && !base.partitioned &&
                             (r->kind == PLAN_DENSE || r->kind == PLAN_HASH) && !(sel_env && !strcmp(sel_env, "never"));
   if (sel_eligible) {
     // Cost in time, not bytes: a pass over a tile costs per-doc work as well as bytes (measured on one
@@ -2463,7 +2574,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (int si : L.segs) {
       DevSegment ds = hsegs[si];
       ds.tile_begin = tiles;
-      ds.key_seg = key_seg[si];
+      ds.key_seg = r->admit ? si : key_seg[si];
       tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
       L.docs += segs[si]->num_docs;
       ls.push_back(ds);
@@ -2562,6 +2673,38 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     L.jit = jit_get(jp, &r->jit_status);
     if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
+    if (r->admit) {
+      // the admission's first-doc pass: the launch's filter + group key over each segment's prefix
+      JitPlan jf = jp;
+      jf.firstdoc = true;
+      jf.admit = jf.lds = jf.partitioned = jf.select = jf.word_select = jf.atomic_gate = jf.sample = false;
+      jf.part_sampled = false;
+      jf.aggregate = false;
+      jf.scan_nsub = 1;
+      jf.vals.clear();
+      jf.val_bits.clear();
+      jf.val_off.clear();
+      jf.rec_bytes = jf.stage_cap = jf.nparts = jf.key_shift = 0;
+      for (auto& lf : jf.leaves) lf.lds_words = 0;
+      L.jit_fd = jit_get(jf, &r->jit_status);
+      if (!L.jit_fd) return fail(PINOT_AMD_EUNSUPPORTED, "first-doc kernel unavailable: %s", r->jit_status.c_str());
+      std::vector<DevSegment> fs;
+      int64_t ftiles = 0;
+      for (size_t k = 0; k < L.segs.size(); ++k) {
+        DevSegment d = ls[k];
+        d.num_docs = r->a_prefix[L.segs[k]];
+        d.tile_begin = ftiles;
+        ftiles += (d.num_docs + kTileDocs - 1) / kTileDocs;
+        fs.push_back(d);
+      }
+      if (int rc = L.d_fd_segs.alloc_copy(fs.data(), fs.size() * sizeof(DevSegment), 0)) return rc;
+      L.fd_q = L.q;
+      L.fd_q.total_tiles = ftiles;
+      int nf = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nf, L.jit_fd->fn, kBlock, 0) != hipSuccess || nf < 1) nf = 1;
+      L.fd_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, ftiles));
+      L.fd_full_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, tiles));
+    }
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
     L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : 0;
     for (const JitLeaf& jl : jp.leaves) L.shmem_sets += (size_t)jl.lds_words * 4;
@@ -2768,6 +2911,41 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   } else {
     if (int rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * (size_t)std::max<int64_t>(num_keys, 1) * 8)) return rc;
   }
+  if (r->admit) {
+    int64_t max_docs = 0;
+    std::vector<int64_t> bb;
+    for (int si = 0; si < n; ++si) {
+      bb.push_back(r->a_buckets);
+      const int64_t nb = (segs[si]->num_docs + 1023) / 1024 + 1;
+      r->a_buckets += nb;
+      r->a_max_buckets = std::max(r->a_max_buckets, nb);
+      max_docs = std::max(max_docs, segs[si]->num_docs);
+    }
+    bb.push_back(r->a_buckets);
+    r->a_cap = std::max<int64_t>(1, std::min<int64_t>(max_docs, num_keys));
+    r->a_words = (num_keys + 31) / 32;
+    if (int rc = r->a_first.alloc((size_t)n * (size_t)num_keys * 4)) return rc;
+    HIP_OK(hipMemset(r->a_first.p, 0xFF, r->a_first.n));  // unseen; the admission resets what it touches
+    if (int rc = r->a_seen.alloc((size_t)n * (size_t)r->a_cap * 4)) return rc;
+    if (int rc = r->a_seen_n.alloc((size_t)n * 8)) return rc;
+    if (int rc = r->a_bits.alloc((size_t)n * (size_t)r->a_words * 4)) return rc;
+    if (int rc = r->a_hist.alloc((size_t)r->a_buckets * 4)) return rc;
+    if (int rc = r->a_bbase.alloc_copy(bb.data(), bb.size() * 8, 0)) return rc;
+    if (int rc = r->a_bstar.alloc((size_t)n * 8)) return rc;
+    if (int rc = r->a_rank.alloc((size_t)n * 8)) return rc;
+    if (int rc = r->a_dstar.alloc((size_t)n * 8)) return rc;
+    if (int rc = r->a_bitmap.alloc((size_t)n * 16 * 8)) return rc;
+    for (auto& L : r->launches) {
+      for (DevQuery* dq : {&L.q, &L.fd_q}) {
+        dq->admit = (const uint32_t*)r->a_bits.p;
+        dq->admit_words = r->a_words;
+        dq->first = (uint32_t*)r->a_first.p;
+        dq->seen = (uint32_t*)r->a_seen.p;
+        dq->seen_n = (unsigned long long*)r->a_seen_n.p;
+        dq->seen_cap = r->a_cap;
+      }
+    }
+  }
   HIP_OK(hipEventCreate(&r->ev0));
   HIP_OK(hipEventCreate(&r->ev1));
   if (int rc = run_plan(r)) return rc;
@@ -2877,6 +3055,7 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
       info += L.word_select ? "-wselect" : "-select";  // wselect: the filter ran on 64-doc words
       break;
     }
+  if (r->admit) info += "+admit";
   if (r->launches.size() > 1) info += " x" + std::to_string(r->launches.size());
   return info.c_str();
 }

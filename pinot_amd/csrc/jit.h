@@ -98,6 +98,11 @@ struct JitPlan {
   // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;
+  // dense numGroupsLimit trimming: the aggregation (and partition count / scatter) drops docs whose key
+  // the segment did not admit (DevQuery::admit); firstdoc: the admission's first-doc pass instead of an
+  // aggregation (filter + group key -> atomicMin of the docId, keys seen first appended per segment)
+  bool admit = false;
+  bool firstdoc = false;
   // ... whose filter reads no column (docId bitsets / ranges / constants only): the select pass
   // evaluates the CNF on 64-doc words
   bool word_select = false;

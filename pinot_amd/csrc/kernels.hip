@@ -154,17 +154,19 @@ __global__ void trim_count_kernel(const unsigned long long* keys, int64_t cap, i
 }
 
 // one block per segment; bstar[s] = -1: the segment holds <= limit keys (nothing trimmed)
+// strict (dense admission over a segment prefix): a segment holding exactly `limit` keys is cut at the
+// limit-th first docId too, since keys beyond the prefix may exist; otherwise <= limit keys admit all
 __global__ void __launch_bounds__(256) trim_select_kernel(int64_t limit, const int64_t* bucket_base,
                                                           const uint32_t* hist, const unsigned long long* seg_distinct,
                                                           int64_t* bstar, int64_t* rank,
-                                                          unsigned long long* limit_reached) {
+                                                          unsigned long long* limit_reached, int strict) {
   __shared__ int64_t wtot[4];
   __shared__ int64_t carry;
   const int s = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t nd = (int64_t)seg_distinct[s];
   // GroupByOperator.java:133: numGroupsLimitReached = numGroups >= numGroupsLimit
   if (threadIdx.x == 0 && nd >= limit) atomicOr(limit_reached, 1ull);
-  if (nd <= limit) {
+  if (strict ? nd < limit : nd <= limit) {
     if (threadIdx.x == 0) bstar[s] = -1;
     return;
   }
@@ -228,6 +230,69 @@ __global__ void trim_cutoff_kernel(int32_t nsegs, const int64_t* bstar, const in
     out = bstar[s] * 1024 + w * 64 + __builtin_ctzll(m);
   }
   dstar[s] = out;
+}
+
+// Dense numGroupsLimit admission (key spaces a dense table holds; the same first-seen semantics as the
+// hash trimming above, DictionaryBasedGroupKeyGenerator.java:351-363). The first-doc pass (JIT,
+// MODE_FIRSTDOC) over a prefix of each segment leaves first[s * nk + key] = the key's first matching
+// docId and the list seen[s * cap ..] of the keys it saw (seen_n[s] of them). Then, over those lists only:
+//   admit_hist:   histogram of first docIds in 1024-doc buckets per segment (LDS, one block per chunk)
+//   trim_select:  the bucket and rank of the limit-th first docId (strict: exactly `limit` keys seen in a
+//                 prefix still cut there)
+//   admit_bucket: that bucket's first docIds as a 1024-bit map; trim_cutoff: the limit-th first docId dstar
+//   admit_bits:   bit key of segment s's bitmap = first <= dstar[s] (all ones when nothing is cut), and
+//                 first[] reset to "unseen" for the next execution
+__global__ void __launch_bounds__(256) admit_hist_kernel(const uint32_t* first, int64_t nk, const uint32_t* seen,
+                                                         const unsigned long long* seen_n, int64_t cap, int64_t chunk,
+                                                         const int64_t* bucket_base, uint32_t* hist) {
+  extern __shared__ uint32_t lh[];
+  const int s = blockIdx.y;
+  const int64_t n = (int64_t)min((unsigned long long)cap, seen_n[s]);
+  const int64_t b0 = bucket_base[s], nb = bucket_base[s + 1] - b0;
+  const int64_t i0 = (int64_t)blockIdx.x * chunk;
+  if (i0 >= n) return;
+  const int64_t i1 = min(n, i0 + chunk);
+  for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = 0u;
+  __syncthreads();
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const uint32_t f = first[(int64_t)s * nk + seen[(int64_t)s * cap + i]];
+    atomicAdd(&lh[min((int64_t)(f >> 10), nb - 1)], 1u);
+  }
+  __syncthreads();
+  for (int64_t b = threadIdx.x; b < nb; b += blockDim.x)
+    if (lh[b]) atomicAdd(&hist[b0 + b], lh[b]);
+}
+
+__global__ void admit_bucket_kernel(const uint32_t* first, int64_t nk, const uint32_t* seen,
+                                    const unsigned long long* seen_n, int64_t cap, int32_t nsegs, const int64_t* bstar,
+                                    unsigned long long* bitmap) {
+  const int s = blockIdx.y;
+  if (s >= nsegs || bstar[s] < 0) return;
+  const int64_t n = (int64_t)min((unsigned long long)cap, seen_n[s]);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = first[(int64_t)s * nk + seen[(int64_t)s * cap + i]];
+    if ((int64_t)(f >> 10) == bstar[s]) atomicOr(&bitmap[(int64_t)s * 16 + ((f & 1023u) >> 6)], 1ull << (f & 63u));
+  }
+}
+
+// one block row per segment: untrimmed segments get every bit; trimmed ones the keys whose first docId
+// is <= dstar (words zeroed by the host first); first[] entries of the listed keys go back to unseen
+__global__ void admit_bits_kernel(uint32_t* first, int64_t nk, const uint32_t* seen, const unsigned long long* seen_n,
+                                  int64_t cap, const int64_t* dstar, uint32_t* admit, int64_t words) {
+  const int s = blockIdx.y;
+  uint32_t* A = admit + (int64_t)s * words;
+  const int64_t n = (int64_t)min((unsigned long long)cap, seen_n[s]);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (dstar[s] == INT64_MAX) {
+    for (int64_t w = t; w < words; w += stride) A[w] = ~0u;
+  }
+  for (int64_t i = t; i < n; i += stride) {
+    const uint32_t key = seen[(int64_t)s * cap + i];
+    uint32_t* f = first + (int64_t)s * nk + key;
+    if (dstar[s] != INT64_MAX && (int64_t)*f <= dstar[s]) atomicOr(&A[key >> 5], 1u << (key & 31u));
+    *f = 0xFFFFFFFFu;
+  }
 }
 
 // Fold a scan table into the final table: every present entry (admitted by the trim cutoff when
@@ -1011,10 +1076,35 @@ hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, 
   hipLaunchKernelGGL(trim_count_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw_seg, acc, fd_acc, bucket_base, hist,
                      seg_distinct);
   hipLaunchKernelGGL(trim_select_kernel, dim3((unsigned)nsegs), dim3(256), 0, st, limit, bucket_base, hist,
-                     seg_distinct, bstar, rank, limit_reached);
+                     seg_distinct, bstar, rank, limit_reached, 0);
   hipLaunchKernelGGL(trim_bitmap_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw_seg, acc, fd_acc, bstar, bitmap);
   hipLaunchKernelGGL(trim_cutoff_kernel, dim3(grid_for(nsegs, kBlock)), dim3(kBlock), 0, st, nsegs, bstar, rank, bitmap,
                      dstar);
+  return hipGetLastError();
+}
+
+hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const unsigned long long* seen_n, int64_t cap,
+                        int32_t nsegs, int64_t limit, const int64_t* bucket_base, int64_t max_buckets, uint32_t* hist,
+                        int64_t* bstar, int64_t* rank, unsigned long long* bitmap, int64_t* dstar,
+                        unsigned long long* limit_reached, int phase, uint32_t* admit, int64_t words, hipStream_t st) {
+  if (nsegs <= 0) return hipSuccess;
+  if (phase == 0) {  // histogram + the limit-th bucket per segment (seen_n doubles as the distinct count)
+    const int64_t chunk = 8192;
+    const unsigned cx = (unsigned)std::max<int64_t>(1, (cap + chunk - 1) / chunk);
+    hipLaunchKernelGGL(admit_hist_kernel, dim3(cx, (unsigned)nsegs), dim3(256), (size_t)max_buckets * 4, st, first, nk,
+                       seen, seen_n, cap, chunk, bucket_base, hist);
+    hipLaunchKernelGGL(trim_select_kernel, dim3((unsigned)nsegs), dim3(256), 0, st, limit, bucket_base, hist, seen_n, bstar,
+                       rank, limit_reached, 1);
+    return hipGetLastError();
+  }
+  const unsigned cx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((cap + 255) / 256, 64));
+  hipLaunchKernelGGL(admit_bucket_kernel, dim3(cx, (unsigned)nsegs), dim3(256), 0, st, first, nk, seen, seen_n, cap, nsegs,
+                     bstar, bitmap);
+  hipLaunchKernelGGL(trim_cutoff_kernel, dim3(grid_for(nsegs, kBlock)), dim3(kBlock), 0, st, nsegs, bstar, rank, bitmap,
+                     dstar);
+  const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((std::max(cap, words) + 255) / 256, 64));
+  hipLaunchKernelGGL(admit_bits_kernel, dim3(bx, (unsigned)nsegs), dim3(256), 0, st, first, nk, seen, seen_n, cap, dstar,
+                     admit, words);
   return hipGetLastError();
 }
 

@@ -171,3 +171,44 @@ def test_full_size_ssb_sf100_linearity_and_oracle_segment():
         same(full, a, name)
         _, exp = oracle.execute(q, [spot])
         same(ex.execute(q, [segs[0]]).groups(), exp, name + " segment 0")
+
+
+# ------------------------------------------------------------------ configs[2] at full per-GPU size
+@pytest.mark.timeout(900)
+def test_full_size_inverted_sweep_vs_oracle_and_linearity(monkeypatch):
+    """configs[2] at bench scale: 100 segments x 10M rows (the bench's 4 distinct inverted-index segments,
+    each staged 25 times), every selectivity of the sweep under the default cost model (word-level
+    select + gather at 0.01-1 %, the fused forward-index scan at 10-50 %): segments 0 and 99 equal the
+    CPU oracle (which expands the same RoaringBitmaps), the 100-segment result equals the merge of two
+    disjoint subsets, COUNT equals numDocsMatched, and at 1 % the selection-vector and fused plans agree
+    on the whole table."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import engine as E
+    distinct = [datagen.inverted_segment(f"inv{i}", ROWS, seed=i) for i in range(4)]
+    segs = [E.ImmutableSegment(distinct[i % 4]) for i in range(NSEG)]
+    ex = E.ServerQueryExecutor()
+    funcs = ["COUNT", "SUM", "SUM"]
+    for sel in datagen.INVERTED_SELECTIVITIES:
+        q = datagen.inverted_query(sel)
+        full = ex.execute(q, segs)
+        g = full.groups()[()]
+        assert g[0] == full.num_docs_matched()
+        a = ex.execute(q, segs[:41]).groups()[()]
+        b = ex.execute(q, segs[41:]).groups()[()]
+        m = [merge_partial(f, x, y) for f, x, y in zip(funcs, a, b)]
+        assert all(_close(x, y) for x, y in zip(g, m)), (sel, g, m)
+        for i in (0, NSEG - 1):
+            got = ex.execute(q, [segs[i]]).groups()[()]
+            _, exp = oracle.execute(q, [distinct[i % 4]])
+            assert all(_close(x, y) for x, y in zip(got, exp[()])), (sel, i, got, exp)
+        if sel == 0.01:
+            plans = {}
+            for pol in ("always", "never"):
+                monkeypatch.setenv("PINOT_AMD_SELECT", pol)
+                r = ex.execute(q, segs)
+                plans[pol] = (r.kernel_info(), r.groups()[()])
+            monkeypatch.delenv("PINOT_AMD_SELECT")
+            assert "select" in plans["always"][0] and "select" not in plans["never"][0], plans
+            x, y = plans["always"][1], plans["never"][1]
+            assert x[0] == y[0] and x[1] == y[1] and _close(x[2], y[2]), plans

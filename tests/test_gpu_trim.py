@@ -4,8 +4,12 @@
   numGroupsLimit), :651-659): each segment admits group keys in the order its matching docs first reach
   them, until it holds numGroupsLimit keys; later keys are dropped, and GroupByOperator.java:133 flags
   numGroupsLimitReached when a segment holds >= numGroupsLimit keys. The oracle restates the map holder
-  literally (docs in docId order, a hash map of admitted keys); the device runs the trim plan (scan
-  tables keyed by (key, segment) with each entry's first matching docId, a per-segment cutoff, merge).
+  literally (docs in docId order, a hash map of admitted keys). The device runs one of two plans:
+  the dense admission plan for key spaces a dense table holds (first matching docId per (segment, key)
+  over a prefix of each segment, the limit-th first docId per segment, admission bitmaps the aggregation
+  reads; `+admit`), or the hash trim plan (scan tables keyed by (key, segment) with each entry's first
+  matching docId, a per-segment cutoff, merge; `jit-hash-trim`). PINOT_AMD_TRIM_PLAN=hash forces the
+  latter; PINOT_AMD_ADMIT_PREFIX shrinks the admission prefixes so segments are redone whole.
 * Exact integer SUM: INT/LONG sums accumulate in 128 bits on the device and in the oracle and are
   rounded to double once, so LONG values at epoch-nanosecond scale (~1.7e18) neither wrap nor drift.
 """
@@ -41,7 +45,8 @@ def _check(engine, q, bufs, segs, expect_trim=None):
     stats = {}
     nm, og = oracle.execute(qc, bufs, stats=stats)
     if expect_trim is not None:
-        assert ("trim" in res.kernel_info()) == expect_trim, res.kernel_info()
+        info = res.kernel_info()
+        assert ("trim" in info or "admit" in info) == expect_trim, info
     assert res.num_docs_matched() == nm
     assert res.num_groups_limit_reached() == stats.get("num_groups_limit_reached", False)
     assert_same_groups(res.groups(), og, _fsum(qc))
@@ -55,20 +60,37 @@ TRIM_QUERIES = [
 ]
 
 
+@pytest.fixture(params=["admit", "admit-short-prefix", "hash"])
+def trim_plan(request, monkeypatch):
+    if request.param == "hash":
+        monkeypatch.setenv("PINOT_AMD_TRIM_PLAN", "hash")
+    if request.param == "admit-short-prefix":  # prefixes too short: segments are redone whole
+        monkeypatch.setenv("PINOT_AMD_ADMIT_PREFIX", "1024")
+    return request.param
+
+
+def _expect_plan(res, plan):
+    info = res.kernel_info()
+    assert ("hash-trim" in info) if plan == "hash" else ("+admit" in info), (plan, info)
+
+
 @pytest.mark.parametrize("qi", range(len(TRIM_QUERIES)))
 @pytest.mark.parametrize("limit", [1, 7, 100, 999])
-def test_num_groups_limit_trimming_vs_oracle(engine, qi, limit):
+def test_num_groups_limit_trimming_vs_oracle(engine, qi, limit, trim_plan):
     rng = np.random.default_rng(qi * 101 + limit)
     bufs = [random_segment(rng, 20_000 + 3_001 * i, name=f"t{i}", bits_cards=(1000, 143)) for i in range(3)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
     q = f"SET numGroupsLimit = {limit}; " + TRIM_QUERIES[qi]
     res, og, stats = _check(engine, q, bufs, segs, expect_trim=True)
+    _expect_plan(res, trim_plan)
     assert stats["num_groups_limit_reached"]
     # every segment admits at most `limit` keys; the combine is their union
     assert len(og) <= 3 * limit
+    res.execute_again()  # the admission state resets between executions
+    assert_same_groups(res.groups(), og, _fsum(parse_sql(q)))
 
 
-def test_trimming_boundary_counts(engine):
+def test_trimming_boundary_counts(engine, trim_plan):
     """A segment holding exactly numGroupsLimit keys is flagged but loses nothing; one key more and
     the last key to appear is dropped."""
     rng = np.random.default_rng(3)
@@ -84,7 +106,8 @@ def test_trimming_boundary_counts(engine):
 
 
 def test_trimming_in_batches(engine, monkeypatch):
-    """Scan tables limited to a few MiB: segments are trimmed batch by batch and merged."""
+    """Hash trim plan with scan tables limited to a few MiB: segments are trimmed batch by batch and merged."""
+    monkeypatch.setenv("PINOT_AMD_TRIM_PLAN", "hash")
     monkeypatch.setenv("PINOT_AMD_HASH_TABLE_BYTES", str(4 << 20))
     rng = np.random.default_rng(8)
     bufs = [random_segment(rng, 60_000 + 7 * i, name=f"b{i}", bits_cards=(1000, 1000)) for i in range(6)]
@@ -95,7 +118,7 @@ def test_trimming_in_batches(engine, monkeypatch):
     assert_same_groups(res.groups(), og, _fsum(parse_sql(q)))
 
 
-def test_highcard_query_with_default_limit(engine):
+def test_highcard_query_with_default_limit(engine, trim_plan):
     """BASELINE configs[3]'s query without its SET numGroupsLimit: ~1M groups per segment, the
     default limit of 100000 keys per segment applies (Pinot's default-option result)."""
     from pinot_amd import datagen
@@ -103,8 +126,32 @@ def test_highcard_query_with_default_limit(engine):
     bufs = [datagen.highcard_segment(f"hcd{i}", 1_500_000, seed=40 + i) for i in range(2)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
     res, og, stats = _check(engine, q, bufs, segs, expect_trim=True)
+    _expect_plan(res, trim_plan)
     assert stats["num_groups_limit_reached"]
     assert 100_000 <= len(og) <= 200_000
+
+
+def test_admission_skewed_keys_and_untrimmed_segments(engine):
+    """Dense admission where the prefix estimate is wrong: keys concentrated at the start of a segment
+    and new keys only late (the prefix sees too few; the segment is redone whole), next to segments
+    holding fewer keys than the limit (everything admitted) — against the oracle."""
+    rng = np.random.default_rng(21)
+    bufs = []
+    for i, (n, cut, card_early, card_late) in enumerate([(200_000, 150_000, 30, 3000), (50_000, 25_000, 2000, 2000),
+                                                         (30_000, 15_000, 20, 20)]):
+        early = rng.integers(0, card_early, cut)
+        late = rng.integers(0, card_late, n - cut)
+        d = np.concatenate([early, late]).astype(np.int32) * 5 + 1
+        bufs.append(S.build_segment(f"sk{i}", {
+            "d": (d, S.INT, {}),
+            "g": (rng.integers(0, 4, n).astype(np.int32), S.INT, {}),
+            "v": (rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64), S.LONG, {"dictionary": False}),
+        }))
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = "SET numGroupsLimit = 500; SELECT d, g, COUNT(*), SUM(v), MIN(v) FROM t WHERE g < 3 GROUP BY d, g"
+    res, og, stats = _check(engine, q, bufs, segs, expect_trim=True)
+    assert "+admit" in res.kernel_info()
+    assert stats["num_groups_limit_reached"]
 
 
 def test_hash_plan_multi_word_keys_and_segments(engine, monkeypatch):
