@@ -280,6 +280,12 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r);
  * gate only the rows that pass it; plus, per inverted-index leaf, the selected bitmaps' serialized
  * bytes and the dense docId bitset written and read once. */
 int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes);
+/* Host planning time of the execute that built this result, per phase, as "phase=ms;..." (raw_keys:
+ * derived dictionaries of raw GROUP BY columns; leaves: per-segment predicate resolution; keys_probe:
+ * merged key space + the plan-time match-count probe; plan: accumulators, plan kind, descriptors;
+ * jit_alloc: kernel lookup / hipRTC compile, launch descriptors and buffers; launch: enqueueing the first
+ * execution). Diagnostics for cold / cached query latency. */
+const char* pinot_amd_result_plan_timing(pinot_amd_result* r);
 /* Kernel timing of the last execute: device milliseconds of the fused scan kernel, measured with
  * HIP events on the execution stream. */
 int pinot_amd_result_last_kernel_ms(pinot_amd_result* r, double* h_ms);

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1162,6 +1163,8 @@ struct pinot_amd_result {
   DevBuf mkeys, macc, movf;
   int64_t mcap = 0;
   int mnw = 0;
+  // host planning time per phase (pinot_amd_result_plan_timing)
+  std::string plan_timing;
   // result compaction cache (valid until the next execution)
   bool compacted = false;
   int64_t ngroups = 0;
@@ -1814,6 +1817,25 @@ static bool env_is(const char* name, const char* val) {
 
 extern "C" {
 
+// wall-clock milliseconds of the planning phases of one execute (diagnostics: where a cold / cached
+// query's host time goes)
+struct PlanClock {
+  std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  std::string* out;
+  explicit PlanClock(std::string* o) : out(o) { out->clear(); }
+  double lap() {
+    const auto now = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(now - last).count();
+    last = now;
+    return ms;
+  }
+  void mark(const char* phase) {
+    char b[64];
+    snprintf(b, sizeof(b), "%s%s=%.3f", out->empty() ? "" : ";", phase, lap());
+    *out += b;
+  }
+};
+
 static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, int32_t n, void* stream,
                         bool filter_only, pinot_amd_result** out) {
   if (!qq || !segs_in || n < 1 || !out) return fail(PINOT_AMD_EINVAL, "execute: bad arguments");
@@ -1823,6 +1845,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   auto res = std::make_unique<pinot_amd_result>();
   pinot_amd_result* r = res.get();
   r->stream = (hipStream_t)stream;
+  PlanClock clk(&r->plan_timing);
   pinot_amd_query filter_q;
   if (filter_only) filter_q.preds = qq->preds;  // FilterPlanNode only: no projection, no aggregation
   const pinot_amd_query* Qp = filter_only ? &filter_q : qq;
@@ -1843,6 +1866,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   }
   const pinot_amd_query& Q = *Qp;
 
+  clk.mark("raw_keys");
   // ---- slots: columns the kernel must decode ----
   std::vector<std::string> slot_cols;
   auto slot_of = [&](const std::string& name) -> int {
@@ -1919,6 +1943,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   DevQuery& q = r->q;
   memset(&q, 0, sizeof(q));
 
+  clk.mark("leaves");
   // ---- group-by key space: merged dictionaries (union over the batch, dictionary order) ----
   r->num_group_by = (int32_t)Q.group_by.size();
   r->limit = Q.num_groups_limit;
@@ -2013,6 +2038,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   };
 
+  clk.mark("keys_probe");
   // ---- accumulators: acc 0 = COUNT; others grouped by slot; ACC_FIRST_DOC last ----
   // nan_skip: MinMaxRangePair.apply compares with < / >, so NaN never enters the pair (MIN / MAX of
   // an aggregation-only query propagate it like Math.min / Math.max)
@@ -2514,6 +2540,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
 
+  clk.mark("plan");
   // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
   const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
   std::vector<int32_t> key_seg(n, 0);
@@ -2946,9 +2973,11 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
     }
   }
+  clk.mark("jit_alloc");
   HIP_OK(hipEventCreate(&r->ev0));
   HIP_OK(hipEventCreate(&r->ev1));
   if (int rc = run_plan(r)) return rc;
+  clk.mark("launch");
   *out = res.release();
   return 0;
 }
@@ -3464,3 +3493,5 @@ int pinot_amd_result_merge_groups(pinot_amd_result* r, const uint64_t* d_keys, c
     return 0;
   });
 }
+
+const char* pinot_amd_result_plan_timing(pinot_amd_result* r) { return r ? r->plan_timing.c_str() : ""; }

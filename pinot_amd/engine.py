@@ -239,6 +239,11 @@ class QueryResult:
         check(lib().pinot_amd_result_last_kernel_ms(self._h, C.byref(out)), "last_kernel_ms")
         return out.value
 
+    def plan_timing(self) -> Dict[str, float]:
+        """Host planning milliseconds per phase of the execute that built this result."""
+        txt = lib().pinot_amd_result_plan_timing(self._h).decode()
+        return {k: float(v) for k, v in (kv.split("=") for kv in txt.split(";") if kv)}
+
     def algorithmic_bytes(self) -> float:
         """Algorithmic HBM bytes of the last execution (pinot_amd_result_algorithmic_bytes)."""
         out = C.c_double()
@@ -287,8 +292,10 @@ class QueryResult:
         check(lib().pinot_amd_result_merge_groups(self._h, keys.data_ptr(), acc.data_ptr(), keys.shape[0],
                                                   _stream_handle(stream)), "merge_groups")
 
-    def groups(self) -> Dict[tuple, list]:
-        """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation."""
+    def fetch_arrays(self):
+        """The groups as flat arrays straight from the library (pinot_amd_result_fetch): (number of groups,
+        keys [g * num_group_by + j], final values as double [g * num_aggs + a], exact int64 values, MINMAXRANGE
+        pairs or None). groups() turns them into Python values."""
         L = lib()
         ng = C.c_int64()
         check(L.pinot_amd_result_num_groups(self._h, C.byref(ng)), "num_groups")
@@ -308,6 +315,14 @@ class QueryResult:
             got2 = C.c_int64()
             check(L.pinot_amd_result_fetch_intermediate(self._h, n, pairs.ctypes.data_as(C.POINTER(C.c_double)),
                                                         C.byref(got2)), "fetch_intermediate")
+        return got, keys, vals, vals_i, pairs
+
+    def groups(self) -> Dict[tuple, list]:
+        """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation."""
+        L = lib()
+        got, keys, vals, vals_i, pairs = self.fetch_arrays()
+        nk = len(self.qc.group_by)
+        nnat = max(len(self._native_aggs), 1)
         out = {}
         for g in range(got.value):
             key = []
