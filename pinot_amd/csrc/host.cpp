@@ -2664,6 +2664,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         for (auto& jl : jp.leaves) jl.bits_regs = 0;
       }
       if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
+      jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1");
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);

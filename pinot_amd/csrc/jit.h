@@ -63,6 +63,7 @@ struct JitPlan {
   int scan_nsub = 1;           // 256-thread groups per scan block (4 for a table above 40 KiB)
   int depth = 1;               // software-pipeline depth (tiles prefetched ahead), 1..4
   int waves_per_eu = 0;        // > 0: occupancy target handed to the register allocator
+  bool nt_loads = false;       // column loads with the non-temporal hint (streamed once, no cache reuse)
   bool bitset = false;
   bool aggregate = true;
   // direct-atomic scan paired with a partitioned plan: runs only when the count pass found at most
