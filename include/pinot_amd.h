@@ -206,6 +206,17 @@ int pinot_amd_query_set_group_key_values(pinot_amd_query* q, const char* column,
                                          const char* const* h_values_s);
 /* QueryOptions numGroupsLimit (InstancePlanMakerImplV2.DEFAULT_NUM_GROUPS_LIMIT = 100000). */
 int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit);
+/* The server's combine table (GroupByUtils.createIndexedTableForCombineOperator, GroupByUtils.java:104-149;
+ * IndexedTable.finish): with no ORDER BY the result keeps LIMIT groups (the table stops accepting new
+ * ones; here the first LIMIT in ascending key order); with ORDER BY the top
+ * trimSize = max(5 * LIMIT, min_server_group_trim_size) groups by the ORDER BY, sorted (ties in ascending
+ * key order). min_server_group_trim_size <= 0 disables the trim (every group kept when ordered). Replaces
+ * the server-side IndexedTable of GroupByCombineOperator; not set: every group is returned. */
+int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t min_server_group_trim_size,
+                                     int64_t group_trim_threshold);
+/* ORDER BY key of the server table, in order of precedence: kind 0 = group-by column `index` (value
+ * order), kind 1 = aggregation `index` (final value, Double.compare); ascending != 0 for ASC. */
+int pinot_amd_query_add_order_by(pinot_amd_query* q, int32_t kind, int32_t index, int32_t ascending);
 
 /* ------------------------------------------------------------------------------------------------
  * Execution and results (IntermediateResultsBlock / AggregationGroupByResult equivalents).

@@ -104,3 +104,64 @@ def rows(qc, groups: dict) -> list:
         i = hits[-1]
         out.sort(key=lambda r: r[i], reverse=not asc)
     return out[: qc.limit]
+
+
+def _value_order(v):
+    """Sort key of a group-by value in dictionary order: numbers ascending (Double.compare for floating
+    values: -0.0 < 0.0, NaN last), strings in String.compareTo order (UTF-16 code units)."""
+    if isinstance(v, str):
+        return (0, v.encode("utf-16-be"))
+    if isinstance(v, float):
+        if math.isnan(v):
+            return (1, float("inf"), 1)
+        return (1, v, 1 if math.copysign(1.0, v) > 0 else 0)
+    return (1, v, 0)
+
+
+def _final_order(x):
+    """Double.compare order of a final aggregation value."""
+    x = float(x)
+    if math.isnan(x):
+        return (1, 0.0, 0)
+    return (0, x, 1 if math.copysign(1.0, x) > 0 else 0)
+
+
+def server_table(qc, groups: dict) -> dict:
+    """The server's combine table (GroupByUtils.createIndexedTableForCombineOperator, GroupByUtils.java:104-149;
+    IndexedTable.finish) over the combined groups: without ORDER BY the first LIMIT groups (taken in
+    ascending group-key order: the key compares its last group-by column first, each column in dictionary
+    order); with ORDER BY the top trimSize = max(5 * LIMIT, minServerGroupTrimSize) groups by the ORDER BY
+    on final values (ties in ascending key order), none dropped when minServerGroupTrimSize <= 0.
+    Returns the kept groups (a dict in the table's order)."""
+    keys = sorted(groups, key=lambda k: tuple(_value_order(v) for v in reversed(k)))
+    if not qc.order_by:
+        return {k: groups[k] for k in keys[:qc.limit]}
+    targets = qc.order_by_targets()
+    rank = {k: i for i, k in enumerate(keys)}
+
+    def sort_key(k):
+        parts = []
+        for kind, idx, asc in targets:
+            if kind == 0:
+                o = _value_order(k[idx])
+            else:
+                o = _final_order(final(qc.aggregations[idx].func, groups[k][idx]))
+            parts.append(o if asc else _Desc(o))
+        return tuple(parts) + (rank[k],)
+    ordered = sorted(keys, key=sort_key)
+    trim = max(5 * qc.limit, qc.min_server_group_trim_size) if qc.min_server_group_trim_size > 0 else len(ordered)
+    return {k: groups[k] for k in ordered[:trim]}
+
+
+class _Desc:
+    """Reverses the order of a sort key component (descending ORDER BY)."""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def __lt__(self, other):
+        return other.v < self.v
+
+    def __eq__(self, other):
+        return self.v == other.v

@@ -925,6 +925,12 @@ struct pinot_amd_query {
   std::map<std::string, MergedKeyColumn> key_space;
   std::vector<AggSpec> aggs;
   int64_t num_groups_limit = 100000;
+  // server-level IndexedTable of the combine (GroupByUtils.createIndexedTableForCombineOperator):
+  // LIMIT (-1: not set, the whole table), ORDER BY keys, minServerGroupTrimSize, groupTrimThreshold
+  int64_t limit = -1;
+  struct OrderBy { int kind, index, asc; };  // kind 0: group-by column `index`, 1: aggregation `index`
+  std::vector<OrderBy> order_by;
+  int64_t min_trim = 5000, trim_threshold = 1000000;
 };
 
 extern "C" {
@@ -1051,6 +1057,25 @@ int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit) {
   return 0;
 }
 
+int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t min_server_group_trim_size,
+                                     int64_t group_trim_threshold) {
+  if (!q || limit < 0) return fail(PINOT_AMD_EINVAL, "set_result_limit: bad arguments");
+  q->limit = limit;
+  q->min_trim = min_server_group_trim_size;
+  q->trim_threshold = group_trim_threshold;
+  return 0;
+}
+
+int pinot_amd_query_add_order_by(pinot_amd_query* q, int32_t kind, int32_t index, int32_t ascending) {
+  if (!q || (kind != 0 && kind != 1) || index < 0) return fail(PINOT_AMD_EINVAL, "add_order_by: bad arguments");
+  if (kind == 0 && index >= (int32_t)q->group_by.size())
+    return fail(PINOT_AMD_EINVAL, "add_order_by: group-by column %d not in the query", index);
+  if (kind == 1 && index >= (int32_t)q->aggs.size())
+    return fail(PINOT_AMD_EINVAL, "add_order_by: aggregation %d not in the query", index);
+  q->order_by.push_back({kind, index, ascending ? 1 : 0});
+  return 0;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------------
@@ -1163,6 +1188,10 @@ struct pinot_amd_result {
   DevBuf mkeys, macc, movf;
   int64_t mcap = 0;
   int mnw = 0;
+  // server-level IndexedTable (pinot_amd_query_set_result_limit / add_order_by), applied at compaction
+  int64_t srv_limit = -1, srv_min_trim = 5000, srv_trim_threshold = 1000000;
+  std::vector<pinot_amd_query::OrderBy> srv_order;
+  bool srv_trimmed = false;
   // host planning time per phase (pinot_amd_result_plan_timing)
   std::string plan_timing;
   // result compaction cache (valid until the next execution)
@@ -1947,6 +1976,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   // ---- group-by key space: merged dictionaries (union over the batch, dictionary order) ----
   r->num_group_by = (int32_t)Q.group_by.size();
   r->limit = Q.num_groups_limit;
+  r->srv_limit = Q.limit;
+  r->srv_order = Q.order_by;
+  r->srv_min_trim = Q.min_trim;
+  r->srv_trim_threshold = Q.trim_threshold;
   double dense_keys = 1;
   for (size_t j = 0; j < Q.group_by.size(); ++j) {
     const std::string& g = Q.group_by[j];
@@ -3152,6 +3185,8 @@ static int compact_slots(const GroupTable& T, hipStream_t st, DevBuf& idx, int64
   return 0;
 }
 
+static int server_trim(pinot_amd_result* r);
+
 static int compact_groups(pinot_amd_result* r) {
   if (r->compacted) return 0;
   hipStream_t st = r->stream;
@@ -3208,6 +3243,7 @@ static int compact_groups(pinot_amd_result* r) {
     r->ckeys.swap(k2);
     r->cacc.swap(a2);
   }
+  if (int rc = server_trim(r)) return rc;
   r->compacted = true;
   return 0;
 }
@@ -3244,6 +3280,144 @@ static double decode_ordered(uint64_t u, int op) {
   return d;
 }
 
+// final value of aggregation a from a group's accumulator words A (AggregationFunction.extractFinalResult):
+// *v as double, *vi the exact int64 for COUNT / SUMLONG / integer SUM within int64
+static void final_value(const pinot_amd_result* r, const uint64_t* A, int a, double* v_out, int64_t* vi_out) {
+  const int acc = r->agg_acc[a];
+  const int op = r->q.acc_op[acc];
+  const uint64_t w = A[acc];
+  const uint64_t cnt = r->q.nacc ? A[0] : 0;
+  double v;
+  int64_t vi = 0;
+  // exact 128-bit integer sum (lo, hi) -> correctly rounded double
+  auto sum128 = [&](int64_t* exact) -> double {
+    const __int128 s = (__int128)(((unsigned __int128)A[acc + 1] << 64) | (unsigned __int128)w);
+    *exact = (s >= (__int128)INT64_MIN && s <= (__int128)INT64_MAX) ? (int64_t)s : INT64_MIN;
+    return (double)s;
+  };
+  switch (r->agg_type[a]) {
+    case PINOT_AMD_AGG_COUNT:
+      vi = (int64_t)cnt;
+      v = (double)vi;
+      break;
+    case PINOT_AMD_AGG_AVG: {
+      int64_t ex;
+      const double s = op == ACC_SUM_F64 ? ([&] { double d; memcpy(&d, &w, 8); return d; })() : sum128(&ex);
+      v = cnt ? s / (double)cnt : -INFINITY;  // AvgAggregationFunction: empty -> DEFAULT_FINAL_RESULT
+      break;
+    }
+    case PINOT_AMD_AGG_MIN:
+    case PINOT_AMD_AGG_MAX:
+      v = decode_ordered(w, op);
+      break;
+    case PINOT_AMD_AGG_MINMAXRANGE:  // MinMaxRangeAggregationFunction.extractFinalResult: max - min
+      v = decode_ordered(A[r->agg_acc2[a]], ACC_MAX) - decode_ordered(w, ACC_MIN);
+      break;
+    default:
+      if (op == ACC_SUM_F64) {
+        memcpy(&v, &w, 8);
+      } else if (op == ACC_SUM_I128) {
+        v = sum128(&vi);
+      } else {
+        vi = (int64_t)w;
+        v = (double)vi;
+      }
+  }
+  *v_out = v;
+  *vi_out = vi;
+}
+
+// merged-key id of group column j of compacted group g
+static int64_t group_key_id(const pinot_amd_result* r, int64_t g, int j) {
+  const bool hash = r->kind == PLAN_HASH || r->merged;
+  if (hash) {
+    const int nwk = r->merged ? r->mnw : r->nw;
+    return (int64_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) & (((uint64_t)1 << r->pack_bits[j]) - 1));
+  }
+  const int64_t sz = (int64_t)std::max<size_t>(r->keys[j].size(), 1);
+  return ((int64_t)r->ckeys[(size_t)g] / std::max<int64_t>(r->key_stride[j], 1)) % sz;
+}
+
+// Double.compare: -0.0 < 0.0, NaN above everything (the order TableResizer's comparators give doubles)
+static int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  const uint64_t ka = java_double_order(a), kb = java_double_order(b);
+  return ka < kb ? -1 : ka > kb ? 1 : 0;
+}
+
+// The combine's IndexedTable at the server (GroupByUtils.java:104-149, IndexedTable.finish): without
+// ORDER BY the table stops taking new groups at LIMIT (the first LIMIT groups it receives; here the first
+// in ascending key order, which is Pinot's order for one segment with an array-based holder); with ORDER
+// BY it keeps the top trimSize = max(5 * LIMIT, minServerGroupTrimSize) groups by the ORDER BY (ties:
+// ascending key), sorted. Pinot additionally trims to trimSize whenever its table passes trimThreshold =
+// max(groupTrimThreshold, 2 * trimSize) groups while merging segments; with more groups than that the
+// surviving set depends on its merge order (the device result keeps the exact top trimSize).
+static int server_trim(pinot_amd_result* r) {
+  r->srv_trimmed = false;
+  if (r->srv_limit < 0 || r->num_group_by == 0) return 0;
+  const int nacc = std::max(r->q.nacc, 1);
+  const bool hash = r->kind == PLAN_HASH || r->merged;
+  const int nwk = r->merged ? r->mnw : hash ? r->nw : 1;
+  int64_t keep;
+  if (r->srv_order.empty()) {
+    keep = r->srv_limit;
+  } else {
+    keep = r->srv_min_trim > 0 ? std::max<int64_t>(r->srv_limit * 5, r->srv_min_trim) : INT64_MAX;
+  }
+  const int64_t ng = r->ngroups;
+  if (ng <= keep && r->srv_order.empty()) return 0;
+  std::vector<int64_t> perm((size_t)ng);
+  for (int64_t g = 0; g < ng; ++g) perm[(size_t)g] = g;
+  if (!r->srv_order.empty()) {
+    // sort keys per group: merged-key ids for group columns (dictionary order = value order), final values
+    const size_t no = r->srv_order.size();
+    std::vector<double> fv((size_t)ng * no);
+    std::vector<int64_t> kid((size_t)ng * no);
+    for (int64_t g = 0; g < ng; ++g)
+      for (size_t o = 0; o < no; ++o) {
+        const auto& ob = r->srv_order[o];
+        if (ob.kind == 0) {
+          kid[(size_t)g * no + o] = group_key_id(r, g, ob.index);
+        } else {
+          int64_t vi;
+          final_value(r, &r->cacc[(size_t)g * nacc], ob.index, &fv[(size_t)g * no + o], &vi);
+        }
+      }
+    auto less = [&](int64_t a, int64_t b) {
+      for (size_t o = 0; o < no; ++o) {
+        const auto& ob = r->srv_order[o];
+        int c;
+        if (ob.kind == 0) {
+          const int64_t x = kid[(size_t)a * no + o], y = kid[(size_t)b * no + o];
+          c = x < y ? -1 : x > y ? 1 : 0;
+        } else {
+          c = java_double_compare(fv[(size_t)a * no + o], fv[(size_t)b * no + o]);
+        }
+        if (c != 0) return ob.asc ? c < 0 : c > 0;
+      }
+      return a < b;  // ascending key (compacted order)
+    };
+    if (keep < ng) {
+      std::nth_element(perm.begin(), perm.begin() + keep, perm.end(), less);
+      perm.resize((size_t)keep);
+    }
+    std::sort(perm.begin(), perm.end(), less);
+  } else {
+    perm.resize((size_t)keep);
+  }
+  std::vector<uint64_t> k2(perm.size() * nwk), a2(perm.size() * nacc);
+  for (size_t i = 0; i < perm.size(); ++i) {
+    std::copy_n(&r->ckeys[(size_t)perm[i] * nwk], nwk, &k2[i * nwk]);
+    std::copy_n(&r->cacc[(size_t)perm[i] * nacc], nacc, &a2[i * nacc]);
+  }
+  r->ckeys.swap(k2);
+  r->cacc.swap(a2);
+  r->srv_trimmed = (int64_t)perm.size() < ng;
+  r->ngroups = (int64_t)perm.size();
+  return 0;
+}
+
 int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, double* h_values, int64_t* h_values_i64,
                            int64_t* h_num_fetched) {
   if (!r || cap < 0 || !h_num_fetched) return fail(PINOT_AMD_EINVAL, "fetch: bad arguments");
@@ -3256,7 +3430,6 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
                                     (long long)cap);
   for (int64_t g = 0; g < r->ngroups; ++g) {
     const uint64_t* A = &r->cacc[(size_t)g * nacc];
-    const uint64_t cnt = r->q.nacc ? A[0] : 0;
     if (h_keys) {
       int64_t rem = hash ? 0 : (int64_t)r->ckeys[(size_t)g];
       for (int j = 0; j < r->num_group_by; ++j) {
@@ -3277,45 +3450,9 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
       }
     }
     for (int a = 0; a < na; ++a) {
-      const int acc = r->agg_acc[a];
-      const int op = r->q.acc_op[acc];
-      const uint64_t w = A[acc];
       double v;
-      int64_t vi = 0;
-      // exact 128-bit integer sum (lo, hi) -> correctly rounded double
-      auto sum128 = [&](int64_t* exact) -> double {
-        const __int128 s = (__int128)(((unsigned __int128)A[acc + 1] << 64) | (unsigned __int128)w);
-        *exact = (s >= (__int128)INT64_MIN && s <= (__int128)INT64_MAX) ? (int64_t)s : INT64_MIN;
-        return (double)s;
-      };
-      switch (r->agg_type[a]) {
-        case PINOT_AMD_AGG_COUNT:
-          vi = (int64_t)cnt;
-          v = (double)vi;
-          break;
-        case PINOT_AMD_AGG_AVG: {
-          int64_t ex;
-          const double s = op == ACC_SUM_F64 ? ([&] { double d; memcpy(&d, &w, 8); return d; })() : sum128(&ex);
-          v = cnt ? s / (double)cnt : -INFINITY;  // AvgAggregationFunction: empty -> DEFAULT_FINAL_RESULT
-          break;
-        }
-        case PINOT_AMD_AGG_MIN:
-        case PINOT_AMD_AGG_MAX:
-          v = decode_ordered(w, op);
-          break;
-        case PINOT_AMD_AGG_MINMAXRANGE:  // MinMaxRangeAggregationFunction.extractFinalResult: max - min
-          v = decode_ordered(A[r->agg_acc2[a]], ACC_MAX) - decode_ordered(w, ACC_MIN);
-          break;
-        default:
-          if (op == ACC_SUM_F64) {
-            memcpy(&v, &w, 8);
-          } else if (op == ACC_SUM_I128) {
-            v = sum128(&vi);
-          } else {
-            vi = (int64_t)w;
-            v = (double)vi;
-          }
-      }
+      int64_t vi;
+      final_value(r, A, a, &v, &vi);
       if (h_values) h_values[g * na + a] = v;
       if (h_values_i64) h_values_i64[g * na + a] = vi;
     }

@@ -367,10 +367,16 @@ class QueryResult:
 
 
 class ServerQueryExecutor:
-    """Compiles a QueryContext and runs it over a list of HBM-resident segments."""
+    """Compiles a QueryContext and runs it over a list of HBM-resident segments.
 
-    def __init__(self, use_inverted_index: bool = True):
+    server_trim: apply the server's combine table to GROUP BY results like GroupByCombineOperator's
+    IndexedTable (LIMIT groups without ORDER BY; the top max(5 * LIMIT, minServerGroupTrimSize) by the
+    ORDER BY otherwise; pinot_amd_query_set_result_limit). Off by default: every group is returned,
+    which is what a multi-server broker reduce over exact partials wants."""
+
+    def __init__(self, use_inverted_index: bool = True, server_trim: bool = False):
         self.use_inverted_index = use_inverted_index
+        self.server_trim = server_trim
 
     def filter_doc_ids(self, query, segments: Sequence[ImmutableSegment], stream=None) -> List[np.ndarray]:
         """FilterPlanNode -> BlockDocIdSet: ascending matching docIds of each segment (the filter
@@ -465,6 +471,9 @@ class ServerQueryExecutor:
                 if key_space is not None and g in key_space:
                     self._set_key_space(qh, g, first.columns[g].stored_type, key_space[g])
             check(L.pinot_amd_query_set_num_groups_limit(qh, qc.num_groups_limit), "set_num_groups_limit")
+            if self.server_trim and qc.group_by:
+                check(L.pinot_amd_query_set_result_limit(qh, qc.limit, qc.min_server_group_trim_size,
+                                                         qc.group_trim_threshold), "set_result_limit")
             native = []
             agg_slots = []
 
@@ -492,6 +501,12 @@ class ServerQueryExecutor:
                     agg_slots.append(("direct", add(a.func, a.column, a.expr)))
             if not qc.aggregations and qc.group_by:
                 add("COUNT", "*")  # DISTINCT-style group-by still needs the group presence count
+            if self.server_trim and qc.group_by:
+                for kind, idx, asc in qc.order_by_targets():
+                    if kind == 1:  # the library aggregation whose final value orders (AVG: sum / count)
+                        a = qc.aggregations[idx]
+                        idx = add(a.func, a.column, a.expr)
+                    check(L.pinot_amd_query_add_order_by(qh, kind, idx, 1 if asc else 0), "add_order_by")
             arr = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
             rh = C.c_void_p()
             check(L.pinot_amd_execute(qh, arr, len(segments), _stream_handle(stream), C.byref(rh)), "execute")

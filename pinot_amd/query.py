@@ -138,6 +138,27 @@ class QueryContext:
     limit: int
     select_columns: List[str]           # plain columns in the SELECT list (group-by outputs)
     num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT
+    # the server combine table's trim options (QueryOptionsUtils: minServerGroupTrimSize, groupTrimThreshold)
+    min_server_group_trim_size: int = 5000
+    group_trim_threshold: int = 1_000_000
+
+    def order_by_targets(self) -> List[Tuple[int, int, bool]]:
+        """ORDER BY as (kind, index, ascending): kind 0 = group-by column index, 1 = aggregation index
+        (matched by alias or the function text, as the broker's select list does)."""
+        out = []
+        for expr, asc in self.order_by:
+            e = expr.lower().replace(" ", "")
+            hit = None
+            for j, g in enumerate(self.group_by):
+                if e == g.lower():
+                    hit = (0, j)
+            for i, a in enumerate(self.aggregations):
+                if e in (a.name.lower().replace(" ", ""), f"{a.func.lower()}({a.column})".lower().replace(" ", "")):
+                    hit = (1, i)
+            if hit is None:
+                raise ValueError(f"ORDER BY {expr} not in select list")
+            out.append((hit[0], hit[1], asc))
+        return out
 
     @property
     def cnf(self) -> List[List[Leaf]]:
@@ -400,13 +421,18 @@ def _query_options(sql: str):
 
 
 def parse_sql(sql: str) -> QueryContext:
-    """Compile a Pinot SQL query of the supported subset into a QueryContext. The numGroupsLimit
-    query option (QueryOptionsUtils.getNumGroupsLimit) is honoured; other options are ignored."""
+    """Compile a Pinot SQL query of the supported subset into a QueryContext. The numGroupsLimit,
+    minServerGroupTrimSize and groupTrimThreshold query options (QueryOptionsUtils) are honoured; other
+    options are ignored."""
     sql, opts = _query_options(sql)
     qc = _Parser(sql).query()
     for k, v in opts.items():
         if k.lower() == "numgroupslimit":
             qc.num_groups_limit = int(v)
+        elif k.lower() == "minservergrouptrimsize":
+            qc.min_server_group_trim_size = int(v)
+        elif k.lower() == "grouptrimthreshold":
+            qc.group_trim_threshold = int(v)
     return qc
 
 

@@ -1,0 +1,49 @@
+"""The server's combine table on the device (pinot_amd_query_set_result_limit / add_order_by: GroupByUtils
+.createIndexedTableForCombineOperator + IndexedTable.finish) against the oracle's restatement
+(oracle_reduce.server_table): LIMIT groups without ORDER BY; the top max(5 * LIMIT, minServerGroupTrimSize)
+by ORDER BY on group columns and final aggregation values (AVG, MIN, SUM) otherwise; trimming disabled
+with minServerGroupTrimSize <= 0; through the dense and hash plans."""
+import numpy as np
+import pytest
+
+import oracle
+from helpers import random_segment
+from oracle_reduce import server_table
+from pinot_amd.query import parse_sql
+
+pytestmark = pytest.mark.gpu
+
+from test_gpu_parity import assert_same_groups  # noqa: E402
+
+QUERIES = [
+    "SELECT d0, COUNT(*), SUM(r_long) FROM t WHERE r_int > 0 GROUP BY d0 LIMIT 7",
+    "SET minServerGroupTrimSize = 4; SELECT d0, d1, SUM(r_long), AVG(r_int) FROM t GROUP BY d0, d1 "
+    "ORDER BY SUM(r_long) DESC LIMIT 3",
+    "SET minServerGroupTrimSize = 30; SELECT d1, MIN(r_double), COUNT(*) FROM t GROUP BY d1 "
+    "ORDER BY d1 DESC, MIN(r_double) LIMIT 2",
+    "SET minServerGroupTrimSize = 20; SELECT d0, AVG(r_int), MAX(r_double) FROM t GROUP BY d0 "
+    "ORDER BY AVG(r_int) LIMIT 5",
+    "SET minServerGroupTrimSize = -1; SELECT d1, COUNT(*) FROM t GROUP BY d1 ORDER BY COUNT(*) DESC LIMIT 1",
+]
+
+
+@pytest.mark.parametrize("plan", ["auto", "hash"])
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_server_table_vs_oracle(qi, plan, monkeypatch):
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import engine as E
+    if plan == "hash":
+        monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    rng = np.random.default_rng(50 + qi)
+    bufs = [random_segment(rng, 30_000 + 1_000 * i, name=f"st{i}", bits_cards=(300, 37)) for i in range(3)]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    qc = parse_sql(QUERIES[qi])
+    got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
+    _, full = oracle.execute(qc, bufs)
+    exp = server_table(qc, full)
+    assert len(got) == len(exp) <= len(full)
+    fsum = {i for i, a in enumerate(qc.aggregations) if a.func in ("SUM", "AVG") and a.column == "r_double"}
+    assert_same_groups(got, exp, fsum)
+    if qc.order_by:  # the table is sorted by the ORDER BY
+        assert list(got) == list(exp)
