@@ -16,6 +16,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <new>
 #include <stdexcept>
@@ -216,6 +217,9 @@ struct pinot_amd_segment {
   int64_t num_docs = 0;
   std::map<std::string, std::unique_ptr<Column>> cols;
   int64_t device_bytes = 0;
+  // docs matching a filter (signature of its predicates -> count), counted once by the planner's
+  // filter-only probe: the segment is immutable, so a filter's count never changes
+  std::map<std::string, int64_t> match_cache;
 };
 
 static bool is_float(int t) { return t == T_FLOAT || t == T_DOUBLE; }
@@ -902,6 +906,29 @@ struct PredSpec {
   double lower_d = 0, upper_d = 0;
   std::string lower_s, upper_s;
 };
+
+static std::mutex g_match_mu;  // guards every segment's match_cache (concurrent planners)
+
+// the filter's identity for the segments' match-count cache: every field of every predicate
+static std::string preds_signature(const std::vector<PredSpec>& preds) {
+  std::string sig;
+  char b[96];
+  for (const PredSpec& p : preds) {
+    sig += p.column;
+    snprintf(b, sizeof(b), "|%d.%d.%d.%d|%d%d%d%d|%lld.%lld|", p.type, p.clause, p.negate, p.use_inv, p.lower_unbounded,
+             p.upper_unbounded, p.lower_inclusive, p.upper_inclusive, (long long)p.lower_i, (long long)p.upper_i);
+    sig += b;
+    sig.append((const char*)&p.lower_d, 8).append((const char*)&p.upper_d, 8);
+    sig += p.lower_s + '\x1f' + p.upper_s + '\x1f';
+    for (int64_t v : p.vi) sig.append((const char*)&v, 8);
+    sig += '\x1e';
+    for (double v : p.vd) sig.append((const char*)&v, 8);
+    sig += '\x1e';
+    for (const std::string& v : p.vs) sig += v + '\x1f';
+    sig += '\x1d';
+  }
+  return sig;
+}
 
 struct AggSpec {
   int32_t type;
@@ -2011,15 +2038,35 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   std::vector<int64_t> seg_matched;
   auto probe_matched = [&]() -> int {
     if (!seg_matched.empty()) return 0;
+    // counts cached on the segments (immutable) by an earlier probe of the same filter; the rest probed
+    const std::string sig = preds_signature(Q.preds);
+    seg_matched.assign(n, -1);
+    std::vector<pinot_amd_segment*> todo;
+    std::vector<int> todo_idx;
+    std::unique_lock<std::mutex> lk(g_match_mu);
+    for (int si = 0; si < n; ++si) {
+      auto it = segs[si]->match_cache.find(sig);
+      if (it != segs[si]->match_cache.end()) {
+        seg_matched[si] = it->second;
+      } else {
+        todo.push_back(segs[si]);
+        todo_idx.push_back(si);
+      }
+    }
+    lk.unlock();
+    if (todo.empty()) return 0;
     pinot_amd_query fq;
     fq.preds = Q.preds;
     pinot_amd_result* fr = nullptr;
-    if (int rc = execute_impl(&fq, segs.data(), n, stream, true, &fr)) return rc;
+    if (int rc = execute_impl(&fq, todo.data(), (int32_t)todo.size(), stream, true, &fr)) return rc;
     std::unique_ptr<pinot_amd_result> hold(fr);
-    seg_matched.assign(n, 0);
-    for (int si = 0; si < n; ++si)
-      if (int rc = pinot_amd_bitset_count((const uint64_t*)fr->bitsets[si]->p, segs[si]->num_docs, &seg_matched[si], stream))
-        return rc;
+    for (size_t k = 0; k < todo.size(); ++k) {
+      int64_t c = 0;
+      if (int rc = pinot_amd_bitset_count((const uint64_t*)fr->bitsets[k]->p, todo[k]->num_docs, &c, stream)) return rc;
+      seg_matched[todo_idx[k]] = c;
+      std::lock_guard<std::mutex> g(g_match_mu);
+      todo[k]->match_cache[sig] = c;
+    }
     return 0;
   };
   // numGroupsLimit: a segment can only reach the limit if it can hold that many keys (matching docs
