@@ -2607,11 +2607,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       base.word_select = base.select && wordy && !env_is("PINOT_AMD_WORD_SELECT", "0");
     }
     if (base.select && base.lds) {
-      // gather blocks may add up to ceil(matches / CUs) + 4 x block docs to one LDS table: re-bound the
-      // narrow 64-bit partials for that and keep the table within the LDS
+      // gather blocks walk the selection vector grid-strided (padding included, matches unevenly spread
+      // over its quads): one block may add every match of the batch to its LDS table, so the narrow
+      // 64-bit partials are bounded by all the docs; keep the table within the LDS
       const int64_t scan_min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
       const __int128 scan_bound = (__int128)((all_tiles + scan_min_grid - 1) / scan_min_grid) * kTileDocs;
-      const __int128 gather_bound = (__int128)((all_docs + cus - 1) / cus) + 4 * 256 * base.scan_nsub;
+      const __int128 gather_bound = (__int128)all_docs;
       if (gather_bound > scan_bound) {
         set_narrow(gather_bound);
         lds_bytes = lds_arrays() * std::max<int64_t>(num_keys, 1) * 8;

@@ -47,6 +47,10 @@ def main(ref="/root/reference"):
                 if name.endswith("_v3") and "v3" not in parts and not any(p.endswith(".properties") for p in parts):
                     continue
                 target = os.path.join(dst, *parts)
+                # members of the (untrusted) archive may only land inside this fixture's directory
+                if os.path.isabs(m.name) or ".." in parts or \
+                        not os.path.realpath(target).startswith(os.path.realpath(dst) + os.sep):
+                    raise ValueError(f"tar member {m.name!r} escapes {dst}")
                 os.makedirs(os.path.dirname(target), exist_ok=True)
                 with t.extractfile(m) as src, open(target, "wb") as o:
                     o.write(src.read())
