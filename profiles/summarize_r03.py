@@ -1,0 +1,101 @@
+"""Summarise profiles/profile_r03.sh outputs (gpurun_out/prof3/<workload>/) into profiles/r03/.
+
+    python3 profiles/summarize_r03.py gpurun_out/prof3 profiles/r03
+
+Per workload: kernel_stats_<w>.csv (rocprofv3 --stats copy) and pmc_<w>.json with, per kernel, the mean
+trace duration and the mean of every counter per dispatch; per execution of the query plan (all its
+kernels): HBM read bytes = FETCH_SIZE x 1024 x 2 (MI355X_MICROARCH.md: FETCH_SIZE is in KiB and counts
+half the bytes of wide coalesced streaming reads on gfx950), write bytes = WRITE_SIZE x 1024, against
+the plan's algorithmic bytes (the bench line's bytes_per_row x rows), and the plan's device time."""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+
+def kname(k):
+    return k.split("(")[0].strip()
+
+
+def pmc(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def bench_line(path):
+    lines = [l for l in open(path) if l.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    index = {}
+    for w in sorted(os.listdir(src)):
+        d = os.path.join(src, w)
+        st = os.path.join(d, "trace", "run_kernel_stats.csv")
+        if not os.path.exists(st):
+            continue
+        shutil.copy(st, os.path.join(dst, f"kernel_stats_{w}.csv"))
+        out = {"workload": w, "kernels": {}}
+        tb = bench_line(os.path.join(d, "trace_bench.json"))
+        execs_trace = 2 + tb["warmup"] + tb["steps"]
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))):
+            durs[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        plan = {k: v for k, v in durs.items() if len(v) >= execs_trace - 1 and
+                any(s in k for s in ("pinot", "roaring", "partition", "exclusive", "init_acc", "trim", "hash", "admit",
+                                     "allot", "merge", "pack_sel", "gather", "presence", "bitset"))}
+        # A kernel with more dispatches than executions also ran the planner's filter-only match-count
+        # probe (selection-vector cost model, numGroupsLimit bound): once in the cold execution since the
+        # round-3 probe cache (dispatch 0), twice before it (dispatches 0 and 2). Plan-time work, dropped.
+        def drop_probe(v, execs):
+            extra = len(v) - execs
+            return [x for i, x in enumerate(v) if i not in ((0,) if extra == 1 else (0, 2) if extra == 2 else ())]
+        probes = {k for k, v in plan.items() if len(v) in (execs_trace + 1, execs_trace + 2)}
+        plan = {k: (drop_probe(v, execs_trace) if k in probes else v) for k, v in plan.items()}
+        for k, v in plan.items():
+            out["kernels"][k] = {"trace_dispatches": len(v), "trace_mean_ms": sum(v) / len(v)}
+        per_exec_bytes = {"read": 0.0, "write": 0.0}
+        execs_pmc = None
+        for i in range(1, 10):
+            p = os.path.join(d, f"pmc{i}", "run_counter_collection.csv")
+            if not os.path.exists(p):
+                continue
+            bl = bench_line(os.path.join(d, f"pmc{i}.json"))
+            execs_pmc = 2 + bl["warmup"] + bl["steps"]
+            for k, cs in pmc(p).items():
+                if k not in plan:
+                    continue
+                for c, vals in cs.items():
+                    if k in probes and len(vals) in (execs_pmc + 1, execs_pmc + 2):
+                        vals = drop_probe(vals, execs_pmc)
+                    out["kernels"][k][c] = sum(vals) / len(vals)
+                    if c == "FETCH_SIZE":
+                        per_exec_bytes["read"] += sum(vals) * 1024 * 2 / execs_pmc
+                    elif c == "WRITE_SIZE":
+                        per_exec_bytes["write"] += sum(vals) * 1024 / execs_pmc
+        alg = tb["roofline"]["bytes_per_row"] * tb["config"]["rows_per_gpu"]
+        plan_ms = sum(o["trace_mean_ms"] * o["trace_dispatches"] / execs_trace for o in out["kernels"].values())
+        out["per_execution"] = {
+            "rows": tb["config"]["rows_per_gpu"], "algorithmic_bytes": alg,
+            "hbm_read_bytes": per_exec_bytes["read"], "hbm_write_bytes": per_exec_bytes["write"],
+            "traffic_over_algorithmic": (per_exec_bytes["read"] + per_exec_bytes["write"]) / alg if alg else None,
+            "plan_device_ms_from_trace": plan_ms,
+            "achieved_GBps_from_trace": alg / (plan_ms / 1e3) / 1e9 if plan_ms else None,
+            "bench_kernel_ms_hip_events": tb["roofline"]["kernel_ms"], "bench_frac": tb["roofline"]["frac"],
+            "query": tb["config"]["query"],
+        }
+        with open(os.path.join(dst, f"pmc_{w}.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        index[w] = out["per_execution"]
+    with open(os.path.join(dst, "pmc_index.json"), "w") as f:
+        json.dump(index, f, indent=1)
+    print(json.dumps(index, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
