@@ -318,38 +318,44 @@ class QueryResult:
         return got, keys, vals, vals_i, pairs
 
     def groups(self) -> Dict[tuple, list]:
-        """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation."""
+        """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation.
+        Converted column-wise (numpy -> Python lists, zipped), not group by group."""
         L = lib()
         got, keys, vals, vals_i, pairs = self.fetch_arrays()
+        n = got.value
         nk = len(self.qc.group_by)
         nnat = max(len(self._native_aggs), 1)
-        out = {}
-        for g in range(got.value):
-            key = []
+        kcols = []
+        if nk:
+            karr = keys[:n * nk].reshape(n, nk)
             for j in range(nk):
-                raw = int(keys[g * nk + j])
                 t = self._key_types[j]
+                col = karr[:, j]
                 if t == STRING:
-                    key.append(L.pinot_amd_result_string_key(self._h, j, raw).decode())
+                    names = {int(i): L.pinot_amd_result_string_key(self._h, j, int(i)).decode() for i in np.unique(col)}
+                    kcols.append([names[i] for i in col.tolist()])
                 elif t in (FLOAT, DOUBLE):
-                    key.append(JavaDouble(np.int64(raw).view(np.float64)))
+                    kcols.append([JavaDouble(x) for x in col.view(np.float64).tolist()])
                 else:
-                    key.append(raw)
-            parts = []
-            for a, slot in zip(self.qc.aggregations, self._agg_slots):
-                if slot[0] == "avg":
-                    s = vals[g * nnat + slot[1]]
-                    c = vals_i[g * nnat + slot[2]]
-                    parts.append((float(s), int(c)))
-                elif slot[0] == "range":
-                    o = (g * nnat + slot[1]) * 2
-                    parts.append((float(pairs[o]), float(pairs[o + 1])))
-                elif a.func in ("COUNT", "SUMLONG"):
-                    parts.append(int(vals_i[g * nnat + slot[1]]))
-                else:
-                    parts.append(float(vals[g * nnat + slot[1]]))
-            out[tuple(key)] = parts
-        return out
+                    kcols.append(col.tolist())
+            key_tuples = list(zip(*kcols))
+        else:
+            key_tuples = [()] * n
+        v = vals[:n * nnat].reshape(n, nnat)
+        vi = vals_i[:n * nnat].reshape(n, nnat)
+        acols = []
+        for a, slot in zip(self.qc.aggregations, self._agg_slots):
+            if slot[0] == "avg":
+                acols.append(list(zip(v[:, slot[1]].tolist(), vi[:, slot[2]].tolist())))
+            elif slot[0] == "range":
+                pr = pairs[:n * nnat * 2].reshape(n, nnat, 2)
+                acols.append(list(zip(pr[:, slot[1], 0].tolist(), pr[:, slot[1], 1].tolist())))
+            elif a.func in ("COUNT", "SUMLONG"):
+                acols.append(vi[:, slot[1]].tolist())
+            else:
+                acols.append(v[:, slot[1]].tolist())
+        parts = [list(p) for p in zip(*acols)] if acols else [[] for _ in range(n)]
+        return dict(zip(key_tuples, parts))
 
     def rows(self) -> List[tuple]:
         return reduce_rows(self.qc, self.groups())
