@@ -55,6 +55,9 @@ hipError_t launch_merge_rows(const uint64_t* keys, const uint64_t* acc, int64_t 
 hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, int64_t len, int32_t* out,
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
+size_t derive_dictionary_scratch(int64_t n);
+hipError_t derive_dictionary(const uint8_t* d_be, int type, int64_t n, void* d_scratch, int32_t* d_ids,
+                             uint8_t* d_dict_be, int64_t* h_card, hipStream_t st);
 hipError_t launch_read_raw(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out, hipStream_t st);
 hipError_t launch_chunk_decompress(const uint8_t* src, uint8_t* dst, const void* jobs, int32_t njobs, int32_t* status,
                                    hipStream_t st);
@@ -171,12 +174,6 @@ static uint64_t java_double_order(double v) {
   if (std::isnan(v)) b = 0x7ff8000000000000ull;
   else memcpy(&b, &v, 8);
   return (b >> 63) ? ~b : (b | (1ull << 63));
-}
-static double java_double_from_order(uint64_t k) {
-  uint64_t b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
-  double v;
-  memcpy(&v, &b, 8);
-  return v;
 }
 static bool java_double_less(double a, double b) { return java_double_order(a) < java_double_order(b); }
 
@@ -1547,66 +1544,29 @@ static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& 
   if (c.type == T_STRING) return fail(PINOT_AMD_EUNSUPPORTED, "GROUP BY on raw STRING column %s", col.c_str());
   const int64_t nd = s->num_docs;
   const int vs = value_size(c.type);
-  std::vector<uint8_t> be((size_t)nd * vs);
-  if (nd) HIP_OK(hipMemcpy(be.data(), c.fwd.p, be.size(), hipMemcpyDeviceToHost));
-  std::vector<uint64_t> key((size_t)nd);  // order-preserving key per doc
-  auto parallel = [nd](auto&& body) {  // [d0, d1) ranges over host threads
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, nd / (1 << 16)));
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { body(nd * t / nt, nd * (t + 1) / nt); });
-    for (auto& x : th) x.join();
-  };
-  parallel([&](int64_t d0, int64_t d1) {
-  for (int64_t d = d0; d < d1; ++d) {
-    const uint8_t* p = be.data() + (size_t)d * vs;
-    uint64_t u = 0;
-    for (int i = 0; i < vs; ++i) u = (u << 8) | p[i];
-    switch (c.type) {
-      case T_INT: key[d] = (uint64_t)(int64_t)(int32_t)(uint32_t)u ^ (1ull << 63); break;
-      case T_LONG: key[d] = u ^ (1ull << 63); break;
-      case T_FLOAT: { uint32_t b = (uint32_t)u; float f; memcpy(&f, &b, 4); key[d] = java_double_order((double)f); break; }
-      default: { double f; memcpy(&f, &u, 8); key[d] = java_double_order(f); break; }
-    }
-  }
-  });
-  std::vector<uint64_t> uniq(key);
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-  const int32_t card = (int32_t)uniq.size();
+  // on the device (derive.hip): order keys, radix sort, distinct values, dictIds, packed forward index
+  DevBuf scratch, ids, dict_be, packed;
+  if (int rc = scratch.alloc(derive_dictionary_scratch(std::max<int64_t>(nd, 1)))) return rc;
+  if (int rc = ids.alloc((size_t)std::max<int64_t>(nd, 1) * 4)) return rc;
+  if (int rc = dict_be.alloc((size_t)std::max<int64_t>(nd, 1) * vs)) return rc;
+  int64_t card = 0;
+  HIP_OK(derive_dictionary((const uint8_t*)c.fwd.p, c.type, nd, scratch.p, (int32_t*)ids.p, (uint8_t*)dict_be.p, &card,
+                           nullptr));
+  card = std::max<int64_t>(card, 1);
   int bits = 1;
-  while (card > 1 && (1ll << bits) < (int64_t)card) ++bits;  // PinotDataBitSet.getNumBitsPerValue(card - 1)
-  // fixed-bit stream, MSB first (FixedBitSVForwardIndexWriter)
-  std::vector<uint8_t> fb((size_t)((nd * bits + 7) / 8) + 8, 0);
-  uint64_t acc = 0;
-  int nacc = 0;
-  size_t o = 0;
-  parallel([&](int64_t d0, int64_t d1) {  // key -> dictId, in place
-    for (int64_t d = d0; d < d1; ++d)
-      key[d] = (uint64_t)(std::lower_bound(uniq.begin(), uniq.end(), key[d]) - uniq.begin());
-  });
-  for (int64_t d = 0; d < nd; ++d) {
-    const uint64_t id = key[d];
-    acc = (acc << bits) | id;
-    nacc += bits;
-    while (nacc >= 8) { fb[o++] = (uint8_t)(acc >> (nacc - 8)); nacc -= 8; }
-  }
-  if (nacc > 0) fb[o++] = (uint8_t)(acc << (8 - nacc));
-  // dictionary: big-endian fixed-width values in sorted order
-  std::vector<uint8_t> dict((size_t)card * vs);
-  for (int32_t i = 0; i < card; ++i) {
-    uint64_t u;
-    switch (c.type) {
-      case T_INT: case T_LONG: u = uniq[i] ^ (1ull << 63); break;
-      case T_FLOAT: { float f = (float)java_double_from_order(uniq[i]); uint32_t b; memcpy(&b, &f, 4); u = b; break; }
-      default: { double f = java_double_from_order(uniq[i]); memcpy(&u, &f, 8); break; }
-    }
-    for (int b = 0; b < vs; ++b) dict[(size_t)i * vs + b] = (uint8_t)(u >> (8 * (vs - 1 - b)));
-  }
+  while (card > 1 && (1ll << bits) < card) ++bits;  // PinotDataBitSet.getNumBitsPerValue(card - 1)
+  const size_t fb_bytes = (size_t)((nd * bits + 7) / 8);
+  if (int rc = packed.alloc(fb_bytes + 8)) return rc;
+  HIP_OK(hipMemset(packed.p, 0, packed.n));
+  if (nd) HIP_OK(launch_pack_dict_ids((const int32_t*)ids.p, nd, bits, (uint8_t*)packed.p, nullptr));
+  std::vector<uint8_t> fb(fb_bytes + 8, 0), dict((size_t)card * vs, 0);
+  HIP_OK(hipMemcpy(fb.data(), packed.p, fb_bytes, hipMemcpyDeviceToHost));
+  if (nd) HIP_OK(hipMemcpy(dict.data(), dict_be.p, dict.size(), hipMemcpyDeviceToHost));
   pinot_amd_column_spec spec{};
   spec.name = out_name->c_str();
   spec.stored_type = c.type;
   spec.encoding = ENC_FIXED_BIT;
-  spec.cardinality = card;
+  spec.cardinality = (int32_t)card;
   spec.bits_per_element = bits;
   spec.h_fwd = fb.data();
   spec.fwd_size = fb.size();
