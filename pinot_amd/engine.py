@@ -17,6 +17,7 @@ Every computation goes through libpinot_amd.so; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import gc
 import math
 from typing import Dict, List, Optional, Sequence
 
@@ -354,8 +355,15 @@ class QueryResult:
                 acols.append(vi[:, slot[1]].tolist())
             else:
                 acols.append(v[:, slot[1]].tolist())
-        parts = [list(p) for p in zip(*acols)] if acols else [[] for _ in range(n)]
-        return dict(zip(key_tuples, parts))
+        # a million small containers would trigger the cyclic GC over and over (none of them is cyclic)
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            parts = list(map(list, zip(*acols))) if acols else [[] for _ in range(n)]
+            return dict(zip(key_tuples, parts))
+        finally:
+            if was:
+                gc.enable()
 
     def rows(self) -> List[tuple]:
         return reduce_rows(self.qc, self.groups())
