@@ -2705,7 +2705,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         for (auto& jl : jp.leaves) jl.bits_regs = 0;
       }
       if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
-      jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1");
+      // non-temporal column loads for wide-row fused scans (configs[1]: 3.58 -> 3.51 ms per 1B rows); the
+      // narrow SSB select passes measured 1-3 % slower with them
+      jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") || (!env_is("PINOT_AMD_NT_LOADS", "0") && bpr >= 16.0);
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);
