@@ -2706,8 +2706,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
       // non-temporal column loads for wide-row fused scans (configs[1]: 3.58 -> 3.51 ms per 1B rows); the
-      // narrow SSB select passes measured 1-3 % slower with them
-      jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") || (!env_is("PINOT_AMD_NT_LOADS", "0") && bpr >= 16.0);
+      // narrow SSB select passes measured 1-3 % slower with them, the partitioned scatter 10 % slower
+      jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") ||
+                    (!env_is("PINOT_AMD_NT_LOADS", "0") && bpr >= 16.0 && !jp.partitioned && !jp.select);
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);
@@ -2722,6 +2723,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.stage_cap = cap >= 4 ? cap : 0;
       if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
       jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
+      jp.flush_every = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_EVERY", 1)));
     }
     {  // algorithmic bytes: each decoded column once (fixed-bit at its width, raw at its value width)
       for (size_t k = 0; k < L.segs.size(); ++k)

@@ -84,6 +84,7 @@ struct JitPlan {
   int rec_bytes = 0;           // record size: 64-bit words x 8
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
   int flush_pct = 85;          // scatter: a partition is written out once this % of its staging is filled (swept: 85 best)
+  int flush_every = 1;         // scatter: the staged partitions are checked (two block barriers) every n tile steps
   // Sampled capacities instead of the exact count pass: a histogram over every sample_stride-th tile
   // sizes each partition's region (DevPartition::cap); the scatter reserves space with one global
   // atomic per flushed run, records beyond a region's capacity go to the overflow slab, aggregated
