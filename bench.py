@@ -108,13 +108,15 @@ PLAN_KERNELS = {
 
 def plan_kernels(info: str) -> str:
     base = info.split(" ")[0]
-    admit = base.endswith("+admit")
-    base = base.replace("+admit", "")
+    admit = "+admit-seq" if "+admit-seq" in base else "+admit" if "+admit" in base else ""
+    base = base.replace(admit, "")
     k = PLAN_KERNELS.get(base)
     if k is None:
         k = PLAN_KERNELS.get(base.replace("-wselect", "").replace("-select", ""), base)
         k += " via " + PLAN_KERNELS["jit-wselect" if base.endswith("-wselect") else "jit-select"]
-    if admit:
+    if admit == "+admit-seq":
+        k += " + numGroupsLimit admission (pinot_admit_seq: one block per segment prefix, seen keys in LDS)"
+    elif admit:
         k += (" + numGroupsLimit admission (pinot_first_doc over segment prefixes, admit_hist_kernel, trim_select, "
               "admit_bucket_kernel, trim_cutoff, admit_bits_kernel)")
     if " x" in info:

@@ -65,7 +65,7 @@ struct DevSegment {
   int64_t num_docs;
   int64_t tile_begin;      // first tile of this segment in its launch
   int32_t key_seg;         // index of the segment in its trim batch (hash key word of trimming plans)
-  int32_t pad;
+  int32_t pad;             // sequential admission descriptors: 1 = the prefix is the whole segment
   DevColumn cols[kMaxSlots];
   DevLeaf leaves[kMaxLeaves];
 };
@@ -180,6 +180,7 @@ struct DevQuery {
   uint32_t* seen;
   unsigned long long* seen_n;
   int64_t seen_cap;
+  unsigned long long* admit_flag;  // numGroupsLimitReached (the sequential admission pass sets it)
 };
 
 }  // namespace pamd

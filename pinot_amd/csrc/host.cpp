@@ -1136,6 +1136,7 @@ struct Launch {
   // dense numGroupsLimit admission: the first-doc pass over each segment's prefix (d_fd_segs: the
   // launch's segments cut to their prefixes), or over whole segments (d_segs) when a prefix saw too few keys
   JitKernel* jit_fd = nullptr;
+  JitKernel* jit_as = nullptr;  // the sequential admission (key spaces that fit LDS), one block per segment
   DevBuf d_fd_segs;
   DevQuery fd_q{};
   int fd_grid = 1, fd_full_grid = 1;
@@ -1697,6 +1698,15 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   return 0;
 }
 
+static int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+static bool env_is(const char* name, const char* val) {
+  const char* v = getenv(name);
+  return v && strcmp(v, val) == 0;
+}
+
 // Dense numGroupsLimit admission, every execution: the first-doc pass over each segment's prefix, the
 // limit-th first docId per segment, the admission bitmaps. A segment whose prefix saw fewer than
 // numGroupsLimit keys (though the segment may hold more) is redone over whole segments (one host check).
@@ -1728,6 +1738,41 @@ static int run_admission(pinot_amd_result* r, unsigned long long* limit_flag) {
                         (int64_t*)r->a_bstar.p, (int64_t*)r->a_rank.p, nullptr, nullptr, limit_flag, 0, nullptr, 0, st));
     return 0;
   };
+  bool seq = !env_is("PINOT_AMD_ADMIT_SEQ", "0");
+  for (auto& L : r->launches) seq &= L.jit_as != nullptr;
+  if (seq) {
+    // one block per segment walks its prefix in doc order (seen keys in an LDS bitmap) and writes the
+    // segment's admission bitmap; a prefix that ended below the limit (outcome 2) is walked again whole
+    auto seq_pass = [&](bool full) -> int {
+      for (auto& L : r->launches) {
+        if (L.segs.empty()) continue;
+        const DevSegment* sg = (const DevSegment*)(full ? L.d_segs.p : L.d_fd_segs.p);
+        DevQuery aq = L.fd_q;
+        aq.total_tiles = full ? L.q.total_tiles : L.fd_q.total_tiles;
+        aq.seen_cap = r->limit;
+        aq.admit_flag = limit_flag;
+        uint64_t* table = nullptr;
+        uint64_t* const* bits = nullptr;
+        unsigned long long* matched = nullptr;
+        DevHash h{};
+        void* args[] = {(void*)&sg, (void*)&aq, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
+        HIP_OK(hipModuleLaunchKernel(L.jit_as->fn, (unsigned)L.segs.size(), 1, 1, kBlock, 1, 1,
+                                     (unsigned)jit_admitseq_lds(nk), st, args, nullptr));
+      }
+      return 0;
+    };
+    if (int rc = seq_pass(false)) return rc;
+    std::vector<unsigned long long> out((size_t)n);
+    HIP_OK(hipMemcpyAsync(out.data(), r->a_seen_n.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    bool again = false;
+    for (int32_t si = 0; si < n; ++si) again |= out[si] == 2;
+    if (again) {
+      HIP_OK(hipMemsetAsync(limit_flag, 0, 8, st));
+      if (int rc = seq_pass(true)) return rc;
+    }
+    return 0;
+  }
   if (int rc = first_pass(false)) return rc;
   if (int rc = select()) return rc;
   std::vector<unsigned long long> seen((size_t)n);
@@ -1821,14 +1866,6 @@ static int bits_for(int64_t card) {  // PinotDataBitSet.getNumBitsPerValue(card 
   int b = 1;
   while (b < 62 && ((int64_t)1 << b) < card) ++b;
   return b;
-}
-static int64_t env_i64(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
-  return v ? atoll(v) : dflt;
-}
-static bool env_is(const char* name, const char* val) {
-  const char* v = getenv(name);
-  return v && strcmp(v, val) == 0;
 }
 
 extern "C" {
@@ -2643,6 +2680,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       DevSegment ds = hsegs[si];
       ds.tile_begin = tiles;
       ds.key_seg = r->admit ? si : key_seg[si];
+      ds.pad = r->admit ? 1 : 0;  // sequential admission over whole segments: each one walked to its end
       tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
       L.docs += segs[si]->num_docs;
       ls.push_back(ds);
@@ -2761,11 +2799,20 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       for (auto& lf : jf.leaves) lf.lds_words = 0;
       L.jit_fd = jit_get(jf, &r->jit_status);
       if (!L.jit_fd) return fail(PINOT_AMD_EUNSUPPORTED, "first-doc kernel unavailable: %s", r->jit_status.c_str());
+      if (r->q.num_keys <= kAdmitSeqMaxKeys && !env_is("PINOT_AMD_ADMIT_SEQ", "0")) {
+        JitPlan js = jf;
+        js.firstdoc = false;
+        js.admitseq = true;
+        std::string err;
+        L.jit_as = jit_get(js, &err);  // absent: the first-doc admission below serves
+      }
       std::vector<DevSegment> fs;
       int64_t ftiles = 0;
       for (size_t k = 0; k < L.segs.size(); ++k) {
         DevSegment d = ls[k];
         d.num_docs = r->a_prefix[L.segs[k]];
+        // the prefix is the whole segment, or the segment cannot reach the limit (no pass: all admitted)
+        d.pad = (d.num_docs == 0 || d.num_docs >= ls[k].num_docs) ? 1 : 0;
         d.tile_begin = ftiles;
         ftiles += (d.num_docs + kTileDocs - 1) / kTileDocs;
         fs.push_back(d);
@@ -3130,7 +3177,11 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
       info += L.word_select ? "-wselect" : "-select";  // wselect: the filter ran on 64-doc words
       break;
     }
-  if (r->admit) info += "+admit";
+  if (r->admit) {
+    bool seq = !env_is("PINOT_AMD_ADMIT_SEQ", "0");
+    for (auto& L : r->launches) seq &= L.jit_as != nullptr;
+    info += seq ? "+admit-seq" : "+admit";
+  }
   if (r->launches.size() > 1) info += " x" + std::to_string(r->launches.size());
   return info.c_str();
 }

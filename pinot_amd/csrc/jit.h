@@ -12,6 +12,12 @@ namespace pamd {
 
 constexpr int kPartSub = 4;  // partition count / scatter blocks: 4 x 256 threads (one block per CU)
 constexpr int kPartCountRatio = 2;  // count-pass blocks per scatter-pass block (count needs little LDS)
+constexpr int64_t kAdmitSeqMaxKeys = 1 << 20;  // sequential admission: the seen-key bitmap (128 KiB) in LDS
+constexpr int kAdmitSeqSlots = 2048;           // its per-tile hash table of new keys (key, first doc)
+// LDS bytes of the sequential admission kernel for a key space
+inline size_t jit_admitseq_lds(int64_t num_keys) {
+  return (size_t)((num_keys + 31) / 32) * 4 + kAdmitSeqSlots * 8 + 1024 * 4 + 80 * 4;
+}
 
 struct JitSlot {
   int enc;       // ENC_* (the same in every segment of the batch)
@@ -105,6 +111,9 @@ struct JitPlan {
   // aggregation (filter + group key -> atomicMin of the docId, keys seen first appended per segment)
   bool admit = false;
   bool firstdoc = false;
+  // admitseq: the admission as one block per segment walking its prefix in doc order with the segment's
+  // seen-key bitmap in LDS (key spaces of <= kAdmitSeqMaxKeys keys)
+  bool admitseq = false;
   // ... whose filter reads no column (docId bitsets / ranges / constants only): the select pass
   // evaluates the CNF on 64-doc words
   bool word_select = false;

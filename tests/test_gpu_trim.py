@@ -9,7 +9,9 @@
   over a prefix of each segment, the limit-th first docId per segment, admission bitmaps the aggregation
   reads; `+admit`), or the hash trim plan (scan tables keyed by (key, segment) with each entry's first
   matching docId, a per-segment cutoff, merge; `jit-hash-trim`). PINOT_AMD_TRIM_PLAN=hash forces the
-  latter; PINOT_AMD_ADMIT_PREFIX shrinks the admission prefixes so segments are redone whole.
+  latter; PINOT_AMD_ADMIT_PREFIX shrinks the admission prefixes so segments are redone whole. Key
+  spaces of <= 2^20 keys admit with one block per segment walking its prefix in doc order (seen keys in
+  an LDS bitmap); PINOT_AMD_ADMIT_SEQ=0 forces the first-doc admission larger key spaces take.
 * Exact integer SUM: INT/LONG sums accumulate in 128 bits on the device and in the oracle and are
   rounded to double once, so LONG values at epoch-nanosecond scale (~1.7e18) neither wrap nor drift.
 """
@@ -60,12 +62,14 @@ TRIM_QUERIES = [
 ]
 
 
-@pytest.fixture(params=["admit", "admit-short-prefix", "hash"])
+@pytest.fixture(params=["admit", "admit-short-prefix", "admit-firstdoc", "admit-firstdoc-short-prefix", "hash"])
 def trim_plan(request, monkeypatch):
     if request.param == "hash":
         monkeypatch.setenv("PINOT_AMD_TRIM_PLAN", "hash")
-    if request.param == "admit-short-prefix":  # prefixes too short: segments are redone whole
+    if request.param.endswith("short-prefix"):  # prefixes too short: segments are redone whole
         monkeypatch.setenv("PINOT_AMD_ADMIT_PREFIX", "1024")
+    if request.param.startswith("admit-firstdoc"):  # the first-doc admission (key spaces past LDS)
+        monkeypatch.setenv("PINOT_AMD_ADMIT_SEQ", "0")
     return request.param
 
 
