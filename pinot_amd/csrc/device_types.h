@@ -59,6 +59,9 @@ struct DevLeaf {
   const int64_t* in_i;
   const double* in_d;
   int32_t in_n, pad;
+  // dictionary leaves of columns of <= 64 values: bit d set = dictId d passes (LEAF_CONST: all or none;
+  // negation not applied). The accept-mask plans test a doc with one bit extract.
+  uint64_t accept;
 };
 
 struct DevSegment {

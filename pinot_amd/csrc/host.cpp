@@ -1442,9 +1442,17 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
   }
   const bool empty = is_range ? end <= start : ids.empty();
   const bool full = is_range ? (start <= 0 && end >= c.card) : (int64_t)ids.size() == c.card;
+  L->accept = 0ull;
+  if (c.card <= 64) {
+    if (is_range)
+      for (int64_t d = std::max<int64_t>(start, 0); d < std::min<int64_t>(end, c.card); ++d) L->accept |= 1ull << d;
+    else
+      for (int32_t d : ids) L->accept |= 1ull << d;
+  }
   if (empty || full) {  // alwaysFalse / alwaysTrue evaluators
     L->kind = LEAF_CONST;
     L->lo_i = full ? 1 : 0;
+    L->accept = full ? ~0ull : 0ull;
     *needs_slot = false;
     L->slot = -1;
     return 0;
@@ -2719,9 +2727,22 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         if (jl.slot >= 0) small_sets &= d.cols[jl.slot].card < 64 * 32;
       }
       jl.bits_regs = (small_sets && (jl.kinds & (1u << LEAF_DICT_SET))) ? 1 : 0;
+      // accept masks: a dictionary column of <= 64 values in every segment, leaves that are dictId ranges /
+      // sets / constants (one bit extract per doc instead of a range compare or a set lookup)
+      {
+        const uint32_t ok = (1u << LEAF_DICT_RANGE) | (1u << LEAF_DICT_SET) | (1u << LEAF_CONST);
+        int64_t maxc = 0;
+        bool dict = jl.slot >= 0 && ls[0].cols[jl.slot].enc != ENC_RAW;
+        for (auto& d : ls) if (jl.slot >= 0) maxc = std::max<int64_t>(maxc, d.cols[jl.slot].card);
+        if (dict && !(jl.kinds & ~ok) && (jl.kinds & ((1u << LEAF_DICT_RANGE) | (1u << LEAF_DICT_SET))) && maxc <= 64 &&
+            !env_is("PINOT_AMD_LEAF_MASKS", "0")) {
+          jl.mask = maxc <= 32 ? 1 : 2;
+          jl.bits_regs = 0;
+        }
+      }
       // larger dictId sets (<= 4096 words) are read from LDS, not from global memory per doc, by the
       // 256-thread blocks of non-partitioned plans (fused scans with nsub 1, every select pass)
-      if (!jl.bits_regs && jl.slot >= 0 && (jl.kinds & (1u << LEAF_DICT_SET)) && !jp.partitioned &&
+      if (!jl.bits_regs && !jl.mask && jl.slot >= 0 && (jl.kinds & (1u << LEAF_DICT_SET)) && !jp.partitioned &&
           (jp.scan_nsub == 1 || jp.select) && !env_is("PINOT_AMD_LDS_SETS", "0")) {
         int64_t w = 0;
         for (auto& d : ls) w = std::max<int64_t>(w, (d.cols[jl.slot].card >> 5) + 1);

@@ -34,6 +34,9 @@ struct JitLeaf {
   // dictId set of <= lds_words 32-bit words in every segment (too large for lane registers): copied
   // into LDS when the block's segment changes (256-thread blocks only: the segment is block-uniform)
   int lds_words = 0;
+  // 1 / 2: the column has <= 32 / <= 64 dictIds in every segment: the leaf is DevLeaf::accept, tested
+  // per doc with one bit extract, OR-ed with the clause's other mask leaves on the same column first
+  int mask = 0;
 };
 // value an accumulator reads: a column slot, or a binary arithmetic expression of two slots
 // (EXPR_MUL / SUB / ADD: Pinot's times / minus / plus transforms)
