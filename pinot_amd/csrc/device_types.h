@@ -113,13 +113,13 @@ struct DevPartition {
 struct ExpandJob {
   const uint8_t* inv;          // staged inverted-index buffer
   const struct RoaringContainer* conts;  // container directory of the column
-  const int32_t* sel;          // selected container indices, grouped by 65536-doc chunk
-  const int32_t* grp;          // chunk k's containers: sel[grp[k] .. grp[k+1])
+  const int32_t* sel;          // selected container indices, grouped by work item (expand_group() chunks)
+  const int32_t* grp;          // work item k's containers: sel[grp[k] .. grp[k+1])
   unsigned long long* bitset;  // output, nwords 64-bit words (every word written each run)
   int64_t num_docs, nwords;
   int64_t sel_begin;           // prefix of nsel over the plan's jobs
   int64_t item_begin;          // prefix of nchunks over the plan's jobs (work items)
-  int32_t nsel, nchunks;
+  int32_t nsel, nchunks;       // nchunks: the job's work items (groups of expand_group() 65536-doc chunks)
   // the selected containers' descriptors packed in the sel order (byte offset | min(count, 65535) << 32
   // | kind << 48), built once per plan: one load per container instead of sel -> directory; nullptr
   // when the inverted-index buffer is 4 GiB or larger

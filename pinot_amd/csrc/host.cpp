@@ -70,7 +70,9 @@ hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* 
 hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
                                  int32_t* out, hipStream_t st);
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
-hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, unsigned long long* out, hipStream_t st);
+hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int group, unsigned long long* out,
+                           hipStream_t st);
+int expand_group();
 hipError_t launch_partition_offsets(const uint32_t* d_hist, int32_t nparts, int64_t nblocks, int64_t* d_offs,
                                     int64_t* d_part_begin, hipStream_t st);
 hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int mode, int64_t stride, double scale,
@@ -1477,18 +1479,21 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     // chunk of the dense bitset in LDS from its group and writes it out once
     const int64_t tiles = (seg->num_docs + kTileDocs - 1) / kTileDocs;
     const size_t bs_bytes = (size_t)std::max<int64_t>(tiles, 1) * kTileDocs / 8 + 64;
+    // work items: groups of G consecutive chunks; a group's containers in (value, chunk) order
     const int32_t nchunks = (int32_t)((bs_bytes / 8 + 1023) / 1024);
-    std::vector<int32_t> grp(nchunks + 1, 0);
+    const int32_t G = expand_group();
+    const int32_t ngroups = (nchunks + G - 1) / G;
+    std::vector<int32_t> grp(ngroups + 1, 0);
     for (int32_t d : ids)
       for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k)
-        if (c.inv_keys[k] < nchunks) ++grp[c.inv_keys[k] + 1];
-    for (int32_t k = 0; k < nchunks; ++k) grp[k + 1] += grp[k];
-    std::vector<int32_t> sel(grp[nchunks]);
+        if (c.inv_keys[k] < nchunks) ++grp[c.inv_keys[k] / G + 1];
+    for (int32_t k = 0; k < ngroups; ++k) grp[k + 1] += grp[k];
+    std::vector<int32_t> sel(grp[ngroups]);
     {
       std::vector<int32_t> fillp(grp.begin(), grp.end() - 1);
       for (int32_t d : ids)
         for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k)
-          if (c.inv_keys[k] < nchunks) sel[fillp[c.inv_keys[k]]++] = (int32_t)k;
+          if (c.inv_keys[k] < nchunks) sel[fillp[c.inv_keys[k] / G]++] = (int32_t)k;
     }
     auto bs = std::make_unique<DevBuf>();
     int rc = bs->alloc(bs_bytes);
@@ -1501,13 +1506,13 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     if (rc) return rc;
     double sel_bytes = 0;
     for (int32_t d : ids) sel_bytes += (double)(c.inv_bytes[d + 1] - c.inv_bytes[d]);
-    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), nchunks, seg->num_docs,
+    r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), ngroups, seg->num_docs,
                              sel_bytes + 2.0 * (double)((seg->num_docs + 7) / 8)});
     if (!sel.empty() && c.inv.n < ((size_t)1 << 32)) {  // packed descriptors, built once per plan
       auto pb = std::make_unique<DevBuf>();
       rc = pb->alloc(sel.size() * 8);
       if (rc) return rc;
-      HIP_OK(launch_pack_sel(c.inv_conts.p, (const int32_t*)sb->p, (int64_t)sel.size(), (unsigned long long*)pb->p, st));
+      HIP_OK(launch_pack_sel(c.inv_conts.p, (const int32_t*)sb->p, (int64_t)sel.size(), G, (unsigned long long*)pb->p, st));
       r->inv_leaves.back().psel = pb.get();
       r->owned.push_back(std::move(pb));
     }

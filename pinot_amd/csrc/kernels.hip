@@ -665,8 +665,8 @@ __device__ __forceinline__ RoaringContainer expand_desc(const ExpandJob& J, int3
   if (J.psel) {
     const unsigned long long d = J.psel[ci];
     RoaringContainer c;
-    c.key = 0u;
-    c.kind = (uint32_t)(d >> 48);
+    c.key = (uint32_t)(d >> 50) & 7u;  // the chunk within the item's chunk group
+    c.kind = (uint32_t)(d >> 48) & 3u;
     c.count = (uint32_t)((d >> 32) & 0xFFFFu);
     c.pad = 0u;
     c.offset = d & 0xFFFFFFFFull;
@@ -675,22 +675,30 @@ __device__ __forceinline__ RoaringContainer expand_desc(const ExpandJob& J, int3
   return J.conts[J.sel[ci]];
 }
 
-// Plan time: pack the selected containers' descriptors in sel order (ExpandJob::psel)
-__global__ void pack_sel_kernel(const RoaringContainer* conts, const int32_t* sel, int64_t n, unsigned long long* out) {
+// Plan time: pack the selected containers' descriptors in sel order (ExpandJob::psel): byte offset |
+// min(count, 65535) << 32 | kind << 48 | (key mod group) << 50
+__global__ void pack_sel_kernel(const RoaringContainer* conts, const int32_t* sel, int64_t n, int group,
+                                unsigned long long* out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const RoaringContainer c = conts[sel[i]];
-    out[i] = c.offset | ((unsigned long long)min(c.count, 65535u) << 32) | ((unsigned long long)c.kind << 48);
+    out[i] = c.offset | ((unsigned long long)min(c.count, 65535u) << 32) | ((unsigned long long)c.kind << 48) |
+             ((unsigned long long)(c.key % (uint32_t)group) << 50);
   }
 }
 
 // Batched expansion: every (segment, inverted-index leaf) of a plan is one ExpandJob; a work item
-// is one 65536-doc chunk of one job. A block builds its chunk's 8 KiB of bitset in LDS from the
-// chunk's selected containers (LDS atomics, no global atomics), then writes all 1024 words once
-// (chunks with no container write zeros, so no separate clear pass). Small array containers are
-// expanded one per lane; bitmap, run and large array containers by a whole wave.
+// is a group of G consecutive 65536-doc chunks of one job. A block builds the group's G x 8 KiB of
+// bitset in LDS from its selected containers (LDS atomics, no global atomics), then writes all its
+// words once (chunks with no container write zeros, so no separate clear pass). Small array
+// containers are expanded one per lane; bitmap, run and large array containers by a whole wave.
+// The group's containers are ordered by value, then chunk: a value's containers of consecutive chunks
+// are adjacent in the serialized bitmap (payloads in key order), so neighbouring lanes read neighbouring
+// bytes -- with a few docs per container (selective IN lists), one chunk per item made every container
+// its own cache-line fetch.
+template <int G>
 __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const ExpandJob* jobs, int32_t njobs,
                                                                       int64_t total_items) {
-  __shared__ uint32_t lbits[2048];
+  __shared__ uint32_t lbits[2048 * G];
   constexpr int kPer = 4;  // containers per lane per round: their loads are independent (latency overlap)
   __shared__ int32_t bigq[kBlock * kPer];
   __shared__ int32_t nbig;
@@ -703,7 +711,7 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
     }
     const ExpandJob& J = jobs[lo];
     const int32_t k = (int32_t)(item - J.item_begin);
-    for (int i = tid; i < 2048; i += kBlock) lbits[i] = 0u;
+    for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
     if (tid == 0) nbig = 0;
     __syncthreads();
     const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
@@ -744,9 +752,10 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
       for (int u = 0; u < kPer; ++u) {
         if (si[u] < 0) continue;
         if (c[u].kind == 0 && c[u].count <= 16) {
+          uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c[u].key % (uint32_t)G);
 #pragma unroll
           for (uint32_t e = 0; e < 16; ++e)
-            if (e < c[u].count) atomicOr(&lbits[v[u][e] >> 5], 1u << (v[u][e] & 31));
+            if (e < c[u].count) atomicOr(&lb[v[u][e] >> 5], 1u << (v[u][e] & 31));
         } else {
           bigq[atomicAdd(&nbig, 1)] = si[u];
         }
@@ -756,19 +765,20 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
       for (int qi = wave; qi < nb; qi += kBlock / 64) {
         const RoaringContainer c = expand_desc(J, bigq[qi]);
         const uint8_t* p = J.inv + c.offset;
+        uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c.key % (uint32_t)G);
         if (c.kind == 1) {
           for (int i = lane; i < 1024; i += 64) {
             const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
             if (w) {
-              atomicOr(&lbits[2 * i], (uint32_t)w);
-              atomicOr(&lbits[2 * i + 1], (uint32_t)(w >> 32));
+              atomicOr(&lb[2 * i], (uint32_t)w);
+              atomicOr(&lb[2 * i + 1], (uint32_t)(w >> 32));
             }
           }
         } else if (c.kind == 0) {
           const uint16_t* p16 = reinterpret_cast<const uint16_t*>(p);
           for (uint32_t e = lane; e < c.count; e += 64) {
             const uint32_t d = p16[e];
-            atomicOr(&lbits[d >> 5], 1u << (d & 31));
+            atomicOr(&lb[d >> 5], 1u << (d & 31));
           }
         } else {
           for (uint32_t r = 0; r < c.count; ++r) {
@@ -780,7 +790,7 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
               uint32_t m = ~0u;
               if (w == w0) m &= ~0u << (s0 & 31);
               if (w == w1) m &= ~0u >> (31 - (e0 & 31));
-              atomicOr(&lbits[w], m);
+              atomicOr(&lb[w], m);
             }
           }
         }
@@ -790,8 +800,8 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
       __syncthreads();
     }
     // write the chunk (docs >= num_docs are never set: bitmaps hold only the segment's docIds)
-    const int64_t w_begin = (int64_t)k * 1024;
-    for (int i = tid; i < 1024; i += kBlock) {
+    const int64_t w_begin = (int64_t)k * 1024 * G;
+    for (int i = tid; i < 1024 * G; i += kBlock) {
       const int64_t w = w_begin + i;
       if (w < J.nwords) J.bitset[w] = (unsigned long long)lbits[2 * i] | ((unsigned long long)lbits[2 * i + 1] << 32);
     }
@@ -1220,19 +1230,35 @@ hipError_t launch_allot_prefix(const uint32_t* d_hist, int32_t P, int64_t G, int
   return hipGetLastError();
 }
 
-hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, unsigned long long* out, hipStream_t st) {
+hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int group, unsigned long long* out,
+                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(pack_sel_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const RoaringContainer*)conts, sel, n, out);
+  hipLaunchKernelGGL(pack_sel_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const RoaringContainer*)conts, sel, n,
+                     group, out);
   return hipGetLastError();
+}
+
+// the chunk-group size (1, 2, 4 or 8 chunks per work item; the planner groups the containers the same way)
+int expand_group() {
+  static const int g = [] {
+    const char* e = getenv("PINOT_AMD_EXPAND_GROUP");
+    const int v = e ? atoi(e) : 8;
+    return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }();
+  return g;
 }
 
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st) {
   if (njobs <= 0 || total_items <= 0) return hipSuccess;
   const ExpandJob* jobs = reinterpret_cast<const ExpandJob*>(d_jobs);
   const int64_t blocks = std::min<int64_t>(total_items, 16384);
-  hipLaunchKernelGGL(roaring_expand_chunks_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs,
-                     total_items);
+  switch (expand_group()) {
+    case 8: hipLaunchKernelGGL(roaring_expand_chunks_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs, total_items); break;
+    case 4: hipLaunchKernelGGL(roaring_expand_chunks_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs, total_items); break;
+    case 2: hipLaunchKernelGGL(roaring_expand_chunks_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs, total_items); break;
+    default: hipLaunchKernelGGL(roaring_expand_chunks_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, njobs, total_items); break;
+  }
   return hipGetLastError();
 }
 
