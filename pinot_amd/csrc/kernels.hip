@@ -1239,11 +1239,13 @@ hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int
   return hipGetLastError();
 }
 
-// the chunk-group size (1, 2, 4 or 8 chunks per work item; the planner groups the containers the same way)
+// the chunk-group size (1, 2, 4 or 8 chunks per work item; the planner groups the containers the same way).
+// Swept on configs[2] (profiles/r03/sweep_inv_expand_group.txt): 4 beats 8 (a 64 KiB LDS bitset halves
+// the blocks per CU) and 1 (every small container its own line fetch)
 int expand_group() {
   static const int g = [] {
     const char* e = getenv("PINOT_AMD_EXPAND_GROUP");
-    const int v = e ? atoi(e) : 8;
+    const int v = e ? atoi(e) : 4;
     return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }();
   return g;
