@@ -134,6 +134,12 @@ struct DevBuf {
     if (hipMalloc(&p, n ? n : 1) != hipSuccess) return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
     return 0;
   }
+  // at least len bytes, reusing the buffer when it is large enough (scratch kept across calls)
+  int ensure(size_t len) {
+    if (p && n >= len) return 0;
+    reset();
+    return alloc(len);
+  }
 };
 
 static uint32_t be32(const uint8_t* p) {
@@ -1213,6 +1219,9 @@ struct pinot_amd_result {
   // groups are those of the merged table (keys packed as the hash plan packs them)
   bool merged = false;
   DevBuf mkeys, macc, movf;
+  // group compaction scratch (presence bits, chunk counts, total, slot indices, gathered keys / accumulators),
+  // kept across fetches and executions: a fetch allocates nothing on the device
+  DevBuf c_bits, c_counts, c_total, c_idx, c_okeys, c_oacc;
   int64_t mcap = 0;
   int mnw = 0;
   // server-level IndexedTable (pinot_amd_query_set_result_limit / add_order_by), applied at compaction
@@ -3256,19 +3265,19 @@ static GroupTable group_table(const pinot_amd_result* r) {
   return {false, r->q.num_keys, 1, nullptr, (const uint64_t*)r->acc.p};
 }
 
-// device compaction of a group table's non-empty slots (COUNT != 0), ascending: slot indices in idx
-static int compact_slots(const GroupTable& T, hipStream_t st, DevBuf& idx, int64_t* ng) {
-  DevBuf bits, counts, total;
-  if (int rc = bits.alloc((size_t)((T.slots + 63) / 64 + 1) * 8)) return rc;
+// device compaction of a group table's non-empty slots (COUNT != 0), ascending: slot indices in r->c_idx
+static int compact_slots(pinot_amd_result* r, const GroupTable& T, hipStream_t st, int64_t* ng) {
+  DevBuf &bits = r->c_bits, &counts = r->c_counts, &total = r->c_total, &idx = r->c_idx;
+  if (int rc = bits.ensure((size_t)((T.slots + 63) / 64 + 1) * 8)) return rc;
   HIP_OK(launch_presence_bitset(T.acc, T.slots, (unsigned long long*)bits.p, st));
   const int64_t nc = compact_num_chunks(T.slots);
-  if (int rc = counts.alloc((size_t)nc * 8)) return rc;
-  if (int rc = total.alloc(8)) return rc;
+  if (int rc = counts.ensure((size_t)nc * 8)) return rc;
+  if (int rc = total.ensure(8)) return rc;
   HIP_OK(launch_bitset_count((const uint64_t*)bits.p, T.slots, (int64_t*)counts.p, (int64_t*)total.p, st));
   HIP_OK(hipMemcpyAsync(ng, total.p, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   if (*ng > 0) {
-    if (int rc = idx.alloc((size_t)*ng * 4)) return rc;
+    if (int rc = idx.ensure((size_t)*ng * 4)) return rc;
     HIP_OK(launch_bitset_compact((const uint64_t*)bits.p, T.slots, (const int64_t*)counts.p, (int32_t*)idx.p, st));
   }
   return 0;
@@ -3295,15 +3304,15 @@ static int compact_groups(pinot_amd_result* r) {
   const GroupTable T = group_table(r);
   const bool hash = T.hash;
   const int nwk = T.nwk;
-  DevBuf idx, okeys, oacc;
+  DevBuf &idx = r->c_idx, &okeys = r->c_okeys, &oacc = r->c_oacc;
   int64_t ng = 0;
-  if (int rc = compact_slots(T, st, idx, &ng)) return rc;
+  if (int rc = compact_slots(r, T, st, &ng)) return rc;
   r->ngroups = ng;
-  r->ckeys.assign((size_t)ng * nwk, 0);
-  r->cacc.assign((size_t)ng * nacc, 0);
+  r->ckeys.resize((size_t)ng * nwk);
+  r->cacc.resize((size_t)ng * nacc);
   if (ng > 0) {
-    if (int rc = okeys.alloc((size_t)ng * nwk * 8)) return rc;
-    if (int rc = oacc.alloc((size_t)ng * nacc * 8)) return rc;
+    if (int rc = okeys.ensure((size_t)ng * nwk * 8)) return rc;
+    if (int rc = oacc.ensure((size_t)ng * nacc * 8)) return rc;
     HIP_OK(launch_gather_groups((const int32_t*)idx.p, ng, T.keys, nwk, T.slots, T.acc, nacc, (uint64_t*)okeys.p,
                                 (uint64_t*)oacc.p, st));
     HIP_OK(hipMemcpyAsync(r->ckeys.data(), okeys.p, r->ckeys.size() * 8, hipMemcpyDeviceToHost, st));
@@ -3517,7 +3526,9 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
   const int nwk = r->merged ? r->mnw : hash ? r->nw : 1;
   if (r->ngroups > cap) return fail(PINOT_AMD_EOVERFLOW, "fetch: %lld groups exceed capacity %lld", (long long)r->ngroups,
                                     (long long)cap);
-  for (int64_t g = 0; g < r->ngroups; ++g) {
+  // the groups converted in slices on up to 8 host threads (1M groups: key decode + final values)
+  auto convert = [&](int64_t g0, int64_t g1) {
+  for (int64_t g = g0; g < g1; ++g) {
     const uint64_t* A = &r->cacc[(size_t)g * nacc];
     if (h_keys) {
       int64_t rem = hash ? 0 : (int64_t)r->ckeys[(size_t)g];
@@ -3545,6 +3556,16 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
       if (h_values) h_values[g * na + a] = v;
       if (h_values_i64) h_values_i64[g * na + a] = vi;
     }
+  }
+  };
+  const int64_t ng = r->ngroups;
+  const int nt = ng >= (1 << 17) ? (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (nt <= 1) {
+    convert(0, ng);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(convert, ng * t / nt, ng * (t + 1) / nt);
+    for (auto& t : th) t.join();
   }
   *h_num_fetched = r->ngroups;
   return 0;
@@ -3664,9 +3685,9 @@ int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64
     if (r->kind == PLAN_HASH && kp.nw != r->nw) return fail(PINOT_AMD_EINVAL, "export_groups: key packing mismatch");
     if (int rc = check_overflow(r)) return rc;
     const GroupTable T = group_table(r);
-    DevBuf idx;
+    const DevBuf& idx = r->c_idx;
     int64_t ng = 0;
-    if (int rc = compact_slots(T, r->stream, idx, &ng)) return rc;
+    if (int rc = compact_slots(r, T, r->stream, &ng)) return rc;
     *h_key_words = kp.nw;
     *h_num_acc = export_nacc(r);
     *h_num_groups = ng;
