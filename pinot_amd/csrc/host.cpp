@@ -2752,6 +2752,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
             !env_is("PINOT_AMD_LEAF_MASKS", "0")) {
           jl.mask = maxc <= 32 ? 1 : 2;
           jl.bits_regs = 0;
+          // fixed-bit columns of <= 6 bits in 256-thread scan / select blocks: an LDS accept table per
+          // (clause, column), one lookup per 4 docs (<= 3 bits) or per 2 docs (4-6 bits)
+          const JitSlot& js = jp.slots[jl.slot];
+          if (js.enc == ENC_FIXED_BIT && js.bits >= 1 && js.bits <= 6 && !jp.partitioned &&
+              (jp.scan_nsub == 1 || jp.select) && !env_is("PINOT_AMD_LEAF_LUT", "0"))
+            jl.lut = js.bits <= 3 ? 4 * js.bits : 2 * js.bits;
         }
       }
       // larger dictId sets (<= 4096 words) are read from LDS, not from global memory per doc, by the
@@ -2831,7 +2837,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jf.val_bits.clear();
       jf.val_off.clear();
       jf.rec_bytes = jf.stage_cap = jf.nparts = jf.key_shift = 0;
-      for (auto& lf : jf.leaves) lf.lds_words = 0;
+      for (auto& lf : jf.leaves) lf.lds_words = lf.lut = 0;
       L.jit_fd = jit_get(jf, &r->jit_status);
       if (!L.jit_fd) return fail(PINOT_AMD_EUNSUPPORTED, "first-doc kernel unavailable: %s", r->jit_status.c_str());
       if (r->q.num_keys <= kAdmitSeqMaxKeys && !env_is("PINOT_AMD_ADMIT_SEQ", "0")) {
@@ -2863,6 +2869,16 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
     L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : 0;
     for (const JitLeaf& jl : jp.leaves) L.shmem_sets += (size_t)jl.lds_words * 4;
+    {  // LDS accept tables: one per (clause, column) mask group with a lookup table (jit.cpp's layout)
+      std::vector<std::pair<int, int>> groups;
+      for (const JitLeaf& jl : jp.leaves) {
+        if (!jl.mask || !jl.lut) continue;
+        const std::pair<int, int> g{jl.clause, jl.slot};
+        if (std::find(groups.begin(), groups.end(), g) != groups.end()) continue;
+        groups.push_back(g);
+        L.shmem_sets += (size_t)(((1 << jl.lut) + 3) / 4) * 4;
+      }
+    }
     if (!jp.select) L.shmem += L.shmem_sets;  // a select pass has no table: its sets start at 0
     int per_cu = 1;
     if (jp.partitioned) {

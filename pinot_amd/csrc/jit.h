@@ -37,6 +37,10 @@ struct JitLeaf {
   // 1 / 2: the column has <= 32 / <= 64 dictIds in every segment: the leaf is DevLeaf::accept, tested
   // per doc with one bit extract, OR-ed with the clause's other mask leaves on the same column first
   int mask = 0;
+  // > 0 (mask leaves of a fixed-bit column of <= 6 bits, 256-thread scan / select blocks): the clause's
+  // mask group is looked up in an LDS table of 2^lut bytes, built when the block's segment changes and
+  // indexed by lut bits of the packed column: 4 docs' fields (lut = 4 x bits) or 2 docs' (lut = 2 x bits)
+  int lut = 0;
 };
 // value an accumulator reads: a column slot, or a binary arithmetic expression of two slots
 // (EXPR_MUL / SUB / ADD: Pinot's times / minus / plus transforms)
