@@ -2561,8 +2561,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     return c.enc == ENC_FIXED_BIT ? c.bits / 8.0 : c.enc == ENC_RAW ? (double)value_size(c.type) : 0.0;
   };
   const char* sel_env = getenv("PINOT_AMD_SELECT");
-  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit && !base.partitioned &&
-                            (r->kind == PLAN_DENSE || r->kind == PLAN_HASH) && !(sel_env && !strcmp(sel_env, "never"));
+  // (a partitioned plan qualifies too: when its filter keeps few docs, the gather adds them straight into
+  // the HBM table, where the partitioned plan would hand over to a fused direct-atomic scan of every row)
+  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit &&
+                            (r->kind == PLAN_DENSE || r->kind == PLAN_HASH || r->kind == PLAN_PARTITIONED) &&
+                            !env_is("PINOT_AMD_SELECT_PARTITIONED", base.partitioned ? "0" : "-") &&
+                            !(sel_env && !strcmp(sel_env, "never"));
   if (sel_eligible) {
     // Cost in time, not bytes: a pass over a tile costs per-doc work as well as bytes (measured on one
     // MI355X: a fused scan of narrow SSB rows and the select pass alike take ~1-1.3 ps per doc however
@@ -2624,6 +2628,16 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const double sel_t = std::max(leaf_b / kBw, docs_all * sel_doc) + matches * kGatherDoc + (sel_bytes - leaf_b) / kBw;
       base.select = forced || sel_t < 0.9 * scan_t;
       base.word_select = base.select && wordy && !env_is("PINOT_AMD_WORD_SELECT", "0");
+      if (base.select && base.partitioned) {  // the gather aggregates into the dense HBM table
+        r->kind = PLAN_DENSE;
+        base.partitioned = false;
+        base.key_shift = 0;
+        base.nparts = 0;
+        base.vals.clear();
+        base.val_bits.clear();
+        part_vbase.clear();
+        for (JitAcc& a : base.accs) a.narrow = 0;  // HBM tables take full 128-bit adds
+      }
     }
     if (base.select && base.lds) {
       // gather blocks walk the selection vector grid-strided (padding included, matches unevenly spread

@@ -1,5 +1,5 @@
 # rocprofv3 recipe for the round-3 profiles (GPU box, repo root):
-#   WORKLOADS="scan highcard hcdef" bash profiles/profile_r03.sh      # then: inv0 inv2 ssb10 ssb11
+#   WORKLOADS="scan highcard hcdef" bash profiles/profile_r03.sh      # then: inv0 inv2 ssb10 ssb11 ssb7
 # Per workload: a kernel trace with --stats, then separate PMC passes (FETCH_SIZE; WRITE_SIZE; two SQ
 # sets; TCP atomics), each its own short run. One query per run (bench.py --query-index), so every
 # dispatch of the run belongs to the same plan: executions per run = 2 (cold + cached plan) + warmup +
@@ -17,6 +17,7 @@ args_for() {
     inv2) echo "--workload inverted --segments 40 --query-index 2" ;;
     ssb10) echo "--workload ssb --segments 20 --query-index 10" ;;
     ssb11) echo "--workload ssb --segments 20 --query-index 11" ;;
+    ssb7) echo "--workload ssb --segments 20 --query-index 7" ;;
   esac
 }
 for w in ${WORKLOADS:-scan highcard hcdef inv0 inv2 ssb10 ssb11}; do
