@@ -43,6 +43,7 @@ HC_QUERIES = [
 @pytest.mark.parametrize("n", [1, 5000, 300_007])
 def test_highcard_partitioned_vs_oracle(engine, qi, n, monkeypatch):
     monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
+    monkeypatch.setenv("PINOT_AMD_SELECT_PARTITIONED", "0")  # the partitioned plan even where a select would win
     rng = np.random.default_rng(1000 + qi * 7 + n)
     bufs = random_segment(rng, n, bits_cards=(1000, 1000))
     seg = engine.ImmutableSegment(bufs)
@@ -149,6 +150,7 @@ def test_highcard_sampled_handover(engine, monkeypatch, where, stride):
     the direct-atomic scan. Selective (0.25%), broad (50%) and docId-clustered (sorted `ts`) filters,
     sampling off ("0") and a non-power-of-two stride: identical groups and matched-doc count."""
     monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
+    monkeypatch.setenv("PINOT_AMD_SELECT_PARTITIONED", "0")
     monkeypatch.delenv("PINOT_AMD_ATOMIC_HANDOVER", raising=False)
     if stride is None:
         monkeypatch.delenv("PINOT_AMD_SAMPLE_STRIDE", raising=False)
@@ -162,6 +164,32 @@ def test_highcard_sampled_handover(engine, monkeypatch, where, stride):
          f"WHERE {where} GROUP BY d0, d1")
     res = engine.ServerQueryExecutor().execute(q, segs)
     assert res.kernel_info() == "jit-partitioned"
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
+    res.execute_again()
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("where", ["r_int < -995000", "ts = 25", "r_double > 1e9"])
+def test_highcard_select_into_hbm_table(engine, monkeypatch, where):
+    """A selective filter over a key space too large for LDS: the planner prefers the selection-vector
+    plan, whose gather adds the few matching docs straight into the dense HBM table (instead of the
+    partitioned plan handing over to a fused direct-atomic scan of every row). Identical groups and
+    matched-doc count to the oracle, also on re-execution; PINOT_AMD_SELECT_PARTITIONED=0 keeps the
+    partitioned plan (the tests above)."""
+    monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
+    monkeypatch.delenv("PINOT_AMD_SELECT", raising=False)
+    monkeypatch.delenv("PINOT_AMD_SELECT_PARTITIONED", raising=False)
+    rng = np.random.default_rng(41)
+    bufs = [random_segment(rng, 900_000 + 4099 * i, name=f"s{i}", bits_cards=(1000, 1000), sorted_col=True)
+            for i in range(3)]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = ("SET numGroupsLimit = 2000000; SELECT d0, d1, COUNT(*), SUM(r_int), MIN(r_long), MAX(r_double) FROM t "
+         f"WHERE {where} GROUP BY d0, d1")
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert "select" in res.kernel_info(), res.kernel_info()
     nm, og = oracle.execute(q, bufs)
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)

@@ -91,6 +91,7 @@ def test_sampled_capacities_vs_oracle(engine, monkeypatch, scale, stage_cap, whe
     identical groups to the oracle whatever the capacities."""
     monkeypatch.delenv("PINOT_AMD_PARTITIONED", raising=False)
     monkeypatch.delenv("PINOT_AMD_ATOMIC_HANDOVER", raising=False)
+    monkeypatch.setenv("PINOT_AMD_SELECT_PARTITIONED", "0")  # the partitioned plan's handover, not a select
     monkeypatch.setenv("PINOT_AMD_SAMPLE_STRIDE", "1")
     for var, val in (("PINOT_AMD_PART_CAP_SCALE", scale), ("PINOT_AMD_STAGE_CAP", stage_cap)):
         if val is None:
