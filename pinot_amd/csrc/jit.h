@@ -124,6 +124,7 @@ struct JitPlan {
   // ... whose filter reads no column (docId bitsets / ranges / constants only): the select pass
   // evaluates the CNF on 64-doc words
   bool word_select = false;
+  int wsel_words = 4;  // word-level select: 64-doc words per lane and step (4 or 8; 16 words are one tile)
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);
