@@ -266,25 +266,67 @@ def key_columns(qc) -> list:
     return cols
 
 
+def _value_kind(vals) -> str:
+    """'i' (all Python ints), 'f' (all floats), '-' (none), 'o' (strings / mixed)."""
+    if not vals:
+        return "-"
+    if all(isinstance(v, int) and not isinstance(v, bool) for v in vals):
+        return "i"
+    if all(isinstance(v, float) for v in vals):
+        return "f"
+    return "o"
+
+
+def _gather_numeric(vals, kind: str, group=None) -> list:
+    """Every rank's numeric values, concatenated in rank order, through gather_rows (two RCCL / gloo
+    all-gathers of int64 tensors; doubles travel as their bit patterns, so -0.0 and NaN payloads
+    arrive unchanged)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    arr = np.asarray(vals, dtype=np.int64) if kind == "i" else np.asarray(vals, dtype=np.float64).view(np.int64)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    rows = torch.from_numpy(arr.reshape(-1, 1).copy()).to(dev)
+    out = gather_rows(rows, group).cpu().numpy().reshape(-1)
+    return out.tolist() if kind == "i" else out.view(np.float64).tolist()
+
+
 def global_key_space(segments, group_by: Sequence[str], group=None, executor=None) -> dict:
-    """Union over all ranks of every group-by column's values (one all-gather of the value lists),
-    to install with ServerQueryExecutor.execute(..., key_space=...) so that every rank's dense group
-    table indexes the same groups and merge_result can all-reduce them in place."""
+    """Union over all ranks of every group-by column's values, to install with
+    ServerQueryExecutor.execute(..., key_space=...) so that every rank's dense group table indexes the
+    same groups and merge_result can all-reduce them in place. Numeric columns travel as int64 tensors
+    (one all-gather of counts, one of the padded values: million-value raw key columns never go through
+    pickling); string columns, or ranks disagreeing on a column's value kind, through all_gather_object.
+    The union keeps the first occurrence in rank order."""
     import torch.distributed as dist
     from .query import distinct_value
     mine = {g: local_key_values(segments, g, executor) for g in group_by}
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    parts = [None] * world
+    gathered = {}
     if world > 1:
-        dist.all_gather_object(parts, mine, group=group)
+        kinds = [None] * world
+        dist.all_gather_object(kinds, {g: _value_kind(mine[g]) for g in group_by}, group=group)
+        objs = []
+        for g in group_by:
+            ks = {k[g] for k in kinds} - {"-"}
+            if len(ks) == 1 and ks <= {"i", "f"}:
+                gathered[g] = _gather_numeric(mine[g], ks.pop(), group)
+            elif not ks:
+                gathered[g] = []
+            else:
+                objs.append(g)
+        if objs:
+            parts = [None] * world
+            dist.all_gather_object(parts, {g: mine[g] for g in objs}, group=group)
+            for g in objs:
+                gathered[g] = [v for p in parts for v in p[g]]
     else:
-        parts = [mine]
+        gathered = mine
     out = {}
     for g in group_by:
         u = {}
-        for p in parts:
-            for v in p[g]:
-                u.setdefault(distinct_value(v), v)
+        for v in gathered[g]:
+            u.setdefault(distinct_value(v), v)
         out[g] = list(u.values())
     return out
 

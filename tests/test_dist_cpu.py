@@ -289,3 +289,54 @@ def test_int128_sums_merge_exactly_through_allgather():
     exp = [sum(_rank_sums(r)[k] for r in range(4)) for k in range(n)]
     assert _from_words(merged[n:2 * n], merged[2 * n:3 * n]) == exp
     assert list(merged[:n]) == [sum(1000 + r for r in range(4))] * n
+
+
+class _Col:
+    def __init__(self, values):
+        self.has_dictionary = True
+        self.dict_values = np.asarray(values, dtype=object if isinstance(values[0], str) else None)
+
+
+class _Seg:
+    def __init__(self, cols):
+        self.columns = {k: _Col(v) for k, v in cols.items()}
+
+
+def _key_space_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from pinot_amd import dist as pdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    segs = {
+        0: [_Seg({"i": [3, 1, 2 ** 40], "f": [0.5, -0.0, float("nan")], "s": ["b", "a"]})],
+        1: [_Seg({"i": [1, 7], "f": [0.0, 0.5, 2.5], "s": ["c", "a"]})],
+        2: [],  # a rank without segments
+    }[rank]
+    ks = pdist.global_key_space(segs, ["i", "f", "s"])
+    out.put((rank, ks["i"], [repr(v) for v in ks["f"]], ks["s"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_global_key_space_numeric_tensors_and_strings():
+    """global_key_space on 3 gloo ranks (one without segments): INT values and DOUBLE bit patterns
+    (-0.0 distinct from 0.0, NaN kept) through int64 tensor all-gathers, STRING values through
+    all_gather_object; every rank gets the same union, first occurrence in rank order."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_key_space_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == 3
+    for _, i, f, s in got:
+        assert i == [3, 1, 2 ** 40, 7]
+        assert f == ["0.5", "-0.0", "nan", "0.0", "2.5"]
+        assert s == ["b", "a", "c"]
