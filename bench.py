@@ -100,6 +100,7 @@ PLAN_KERNELS = {
     "jit": "pinot_scan_jit",
     "jit-select": "pinot_select+pinot_gather",
     "jit-wselect": "pinot_select(word-level)+pinot_gather",
+    "jit-fwselect": "roaring_select_kernel (inverted-index expansion + word-level select, one launch)+pinot_gather",
     "jit-partitioned": "pinot_part_scatter+pinot_part_agg (+pinot_part_count, or the direct-atomic pinot_scan_jit on handover)",
     "jit-hash": "pinot_scan_jit (HBM hash table)",
     "jit-hash-trim": "pinot_scan_jit (HBM hash table keyed by segment) + trim_* + hash_merge_kernel",
@@ -112,8 +113,9 @@ def plan_kernels(info: str) -> str:
     base = base.replace(admit, "")
     k = PLAN_KERNELS.get(base)
     if k is None:
-        k = PLAN_KERNELS.get(base.replace("-wselect", "").replace("-select", ""), base)
-        k += " via " + PLAN_KERNELS["jit-wselect" if base.endswith("-wselect") else "jit-select"]
+        k = PLAN_KERNELS.get(base.replace("-fwselect", "").replace("-wselect", "").replace("-select", ""), base)
+        k += " via " + PLAN_KERNELS["jit-fwselect" if base.endswith("-fwselect") else
+                                    "jit-wselect" if base.endswith("-wselect") else "jit-select"]
     if admit == "+admit-seq":
         k += " + numGroupsLimit admission (pinot_admit_seq: one block per segment prefix, seen keys in LDS)"
     elif admit:

@@ -110,6 +110,14 @@ struct DevPartition {
 
 // Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the
 // predicate selects) are OR-ed into a dense docId bitset (BitmapBasedFilterOperator's bitmap OR).
+// one segment of a fused inverted-index select launch (roaring_select_kernel)
+struct FusedSelSeg {
+  int64_t item_begin;          // prefix of the segments' work items (chunk groups) over the launch
+  int32_t seg;                 // the segment's index in the launch (the selection vector's tag)
+  int32_t nitems;
+  int32_t job[kMaxLeaves];     // leaf j's ExpandJob when it is an inverted-index bitset here, else -1
+};
+
 struct ExpandJob {
   const uint8_t* inv;          // staged inverted-index buffer
   const struct RoaringContainer* conts;  // container directory of the column

@@ -70,6 +70,9 @@ hipError_t launch_bitset_count(const uint64_t* bits, int64_t num_docs, int64_t* 
 hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const int64_t* d_chunk_offsets,
                                  int32_t* out, hipStream_t st);
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
+hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t nfs, int64_t total_items, const void* d_segs,
+                                 int32_t nleaves, int32_t nclauses, unsigned long long* sel_entries,
+                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, hipStream_t st);
 hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int group, unsigned long long* out,
                            hipStream_t st);
 int expand_group();
@@ -1134,6 +1137,11 @@ struct Launch {
   bool gated = false;    // an inverted-index gate clause: columns are read only where it passes
   // selection-vector plan (late materialisation): select pass over the filter columns, gather pass
   bool select = false, word_select = false;
+  // fused inverted-index select (roaring_select_kernel): expansion + word-level select in one launch
+  bool fused = false;
+  DevBuf d_fused;  // FusedSelSeg per segment of the launch
+  int32_t nfused = 0, fused_leaves = 0, fused_clauses = 0;
+  int64_t fused_items = 0;
   size_t shmem_sets = 0;  // LDS dictId sets of the scan / select pass (JitLeaf::lds_words)
   int gather_grid = 1, gather_threads = 256;
   double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
@@ -1651,7 +1659,12 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   void* args[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
   if (L.select) {  // select pass (filter columns -> selection vector), then the gather-aggregate pass
     HIP_OK(hipMemsetAsync(L.q.sel_count, 0, 16, st));
-    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, (unsigned)L.shmem_sets, st, args, nullptr));
+    if (L.fused)
+      HIP_OK(launch_roaring_select(r->d_expand_jobs.p, L.d_fused.p, L.nfused, L.fused_items, L.d_segs.p,
+                                   L.fused_leaves, L.fused_clauses, L.q.sel_entries, L.q.sel_count, L.q.sel_cap,
+                                   matched, st));
+    else
+      HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, (unsigned)L.shmem_sets, st, args, nullptr));
     if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
       unsigned long long ctr[2];
       HIP_OK(hipMemcpyAsync(ctr, L.q.sel_count, 16, hipMemcpyDeviceToHost, st));
@@ -1825,7 +1838,9 @@ static int run_plan(pinot_amd_result* r) {
   r->compacted = false;
   HIP_OK(hipEventRecord(r->ev0, st));
   // inverted-index leaves: expand roaring containers into dense doc bitsets
-  if (!r->inv_leaves.empty())
+  bool all_fused = !r->launches.empty();
+  for (auto& L : r->launches) all_fused &= L.fused;
+  if (!r->inv_leaves.empty() && !all_fused)
     HIP_OK(launch_expand_jobs(r->d_expand_jobs.p, (int32_t)r->inv_leaves.size(), r->expand_total, st));
   HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
   const size_t nl = r->launches.size();
@@ -2728,6 +2743,38 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     L.q.nsegs = (int32_t)L.segs.size();
     L.q.total_tiles = tiles;
     if (int rc = L.d_segs.alloc_copy(ls.data(), ls.size() * sizeof(DevSegment), 0)) return rc;
+    if (base.word_select && !env_is("PINOT_AMD_FUSED_INV_SELECT", "0")) {
+      // the launch's segments as work items of G-chunk groups; each inverted-index leaf mapped to its
+      // expansion job (its DevLeaf::bits is the job's bitset buffer)
+      const int G = expand_group();
+      std::vector<FusedSelSeg> fv(ls.size());
+      int64_t items = 0;
+      bool ok = true;
+      for (size_t k = 0; k < ls.size(); ++k) {
+        FusedSelSeg& f = fv[k];
+        memset(&f, 0, sizeof(f));
+        f.item_begin = items;
+        f.seg = (int32_t)k;
+        const int64_t words = (segs[L.segs[k]]->num_docs + kTileDocs - 1) / kTileDocs * (kTileDocs / 64);
+        f.nitems = (int32_t)((words + 1024 * G - 1) / (1024 * G));
+        for (int j = 0; j < kMaxLeaves; ++j) f.job[j] = -1;
+        for (size_t j = 0; j < order.size(); ++j) {
+          if (ls[k].leaves[j].kind != LEAF_DOC_BITSET) continue;
+          for (size_t ii = 0; ii < r->inv_leaves.size(); ++ii)
+            if (r->inv_leaves[ii].bitset->p == (const void*)ls[k].leaves[j].bits) f.job[j] = (int32_t)ii;
+          ok &= f.job[j] >= 0 && r->inv_leaves[f.job[j]].nchunks >= f.nitems;
+        }
+        items += f.nitems;
+      }
+      if (ok) {
+        if (int rc = L.d_fused.alloc_copy(fv.data(), fv.size() * sizeof(FusedSelSeg), 0)) return rc;
+        L.fused = true;
+        L.nfused = (int32_t)fv.size();
+        L.fused_items = items;
+        L.fused_leaves = (int32_t)order.size();
+        L.fused_clauses = base.nclauses;
+      }
+    }
     if (filter_only)
       if (int rc = L.d_bitset_ptrs.alloc_copy(lbits.data(), lbits.size() * sizeof(uint64_t*), 0)) return rc;
 
@@ -3240,7 +3287,8 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
   }
   for (const auto& L : r->launches)
     if (L.select) {
-      info += L.word_select ? "-wselect" : "-select";  // wselect: the filter ran on 64-doc words
+      // wselect: the filter ran on 64-doc words; fwselect: fused with the inverted-index expansion
+      info += L.fused ? "-fwselect" : L.word_select ? "-wselect" : "-select";
       break;
     }
   if (r->admit) {

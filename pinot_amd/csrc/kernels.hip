@@ -695,14 +695,109 @@ __global__ void pack_sel_kernel(const RoaringContainer* conts, const int32_t* se
 // are adjacent in the serialized bitmap (payloads in key order), so neighbouring lanes read neighbouring
 // bytes -- with a few docs per container (selective IN lists), one chunk per item made every container
 // its own cache-line fetch.
+constexpr int kExpandPer = 4;  // containers per lane per round: their loads are independent (latency overlap)
+
+// The selected containers of work item k of job J ORed into lbits (G x 2048 words, zeroed by the
+// caller); bigq / nbig: LDS queue of the containers a whole wave expands (nbig = 0 on entry). Called by
+// the whole block (it synchronises).
+template <int G>
+__device__ __forceinline__ void expand_item(const ExpandJob& J, int32_t k, uint32_t* lbits, int32_t* bigq, int32_t* nbig) {
+  constexpr int kPer = kExpandPer;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
+  for (int32_t base = g0; base < g1; base += kBlock * kPer) {
+    // every load of the round first (selected index, descriptor, small-array payload), then the LDS work
+    int32_t si[kPer];  // position in the job's sel order, -1: none
+    RoaringContainer c[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int32_t ci = base + u * kBlock + tid;
+      si[u] = ci < g1 ? ci : -1;
+      if (si[u] >= 0) c[u] = expand_desc(J, ci);
+    }
+    // a small array's <= 16 two-byte entries with 3 dword-aligned 16-byte loads (48 bytes from the
+    // dword holding the first entry; the staged buffer's zero padding keeps the tail in bounds)
+    uint32_t v[kPer][16];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const bool small = si[u] >= 0 && c[u].kind == 0 && c[u].count <= 16;
+      uint32_t w[12];
+      const uint32_t odd = (uint32_t)(c[u].offset >> 1) & 1u;  // entry 0 in the dword's high half
+      if (small) {
+        const u32x4a4* p4 = reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull));
+        const u32x4a4 a = p4[0], b = p4[1], d = p4[2];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y;
+        w[6] = b.z; w[7] = b.w; w[8] = d.x; w[9] = d.y; w[10] = d.z; w[11] = d.w;
+      }
+#pragma unroll
+      for (uint32_t e = 0; e < 16; ++e) {
+        // 16-bit entry e is halfword e + odd of the aligned dwords (compile-time indices: e is unrolled)
+        const uint32_t x0 = (e & 1u) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
+        const uint32_t x1 = ((e + 1) & 1u) ? (w[(e + 1) >> 1] >> 16) : (w[(e + 1) >> 1] & 0xFFFFu);
+        const uint32_t x = odd ? x1 : x0;
+        v[u][e] = small && e < c[u].count ? x : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      if (si[u] < 0) continue;
+      if (c[u].kind == 0 && c[u].count <= 16) {
+        uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c[u].key % (uint32_t)G);
+#pragma unroll
+        for (uint32_t e = 0; e < 16; ++e)
+          if (e < c[u].count) atomicOr(&lb[v[u][e] >> 5], 1u << (v[u][e] & 31));
+      } else {
+        bigq[atomicAdd(nbig, 1)] = si[u];
+      }
+    }
+    __syncthreads();
+    const int nb = *nbig;
+    for (int qi = wave; qi < nb; qi += kBlock / 64) {
+      const RoaringContainer c = expand_desc(J, bigq[qi]);
+      const uint8_t* p = J.inv + c.offset;
+      uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c.key % (uint32_t)G);
+      if (c.kind == 1) {
+        for (int i = lane; i < 1024; i += 64) {
+          const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
+          if (w) {
+            atomicOr(&lb[2 * i], (uint32_t)w);
+            atomicOr(&lb[2 * i + 1], (uint32_t)(w >> 32));
+          }
+        }
+      } else if (c.kind == 0) {
+        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(p);
+        for (uint32_t e = lane; e < c.count; e += 64) {
+          const uint32_t d = p16[e];
+          atomicOr(&lb[d >> 5], 1u << (d & 31));
+        }
+      } else {
+        for (uint32_t r = 0; r < c.count; ++r) {
+          const uint8_t* q = p + 2 + 4 * r;
+          const uint32_t s0 = q[0] | (q[1] << 8);
+          const uint32_t e0 = s0 + (q[2] | (q[3] << 8));  // inclusive, < 65536
+          const uint32_t w0 = s0 >> 5, w1 = e0 >> 5;
+          for (uint32_t w = w0 + lane; w <= w1; w += 64) {
+            uint32_t m = ~0u;
+            if (w == w0) m &= ~0u << (s0 & 31);
+            if (w == w1) m &= ~0u >> (31 - (e0 & 31));
+            atomicOr(&lb[w], m);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) *nbig = 0;
+    __syncthreads();
+  }
+}
+
 template <int G>
 __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const ExpandJob* jobs, int32_t njobs,
                                                                       int64_t total_items) {
   __shared__ uint32_t lbits[2048 * G];
-  constexpr int kPer = 4;  // containers per lane per round: their loads are independent (latency overlap)
-  __shared__ int32_t bigq[kBlock * kPer];
+  __shared__ int32_t bigq[kBlock * kExpandPer];
   __shared__ int32_t nbig;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   for (int64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
@@ -714,92 +809,8 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
     for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
     if (tid == 0) nbig = 0;
     __syncthreads();
-    const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
-    for (int32_t base = g0; base < g1; base += kBlock * kPer) {
-      // every load of the round first (selected index, descriptor, small-array payload), then the LDS work
-      int32_t si[kPer];  // position in the job's sel order, -1: none
-      RoaringContainer c[kPer];
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const int32_t ci = base + u * kBlock + tid;
-        si[u] = ci < g1 ? ci : -1;
-        if (si[u] >= 0) c[u] = expand_desc(J, ci);
-      }
-      // a small array's <= 16 two-byte entries with 3 dword-aligned 16-byte loads (48 bytes from the
-      // dword holding the first entry; the staged buffer's zero padding keeps the tail in bounds)
-      uint32_t v[kPer][16];
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const bool small = si[u] >= 0 && c[u].kind == 0 && c[u].count <= 16;
-        uint32_t w[12];
-        const uint32_t odd = (uint32_t)(c[u].offset >> 1) & 1u;  // entry 0 in the dword's high half
-        if (small) {
-          const u32x4a4* p4 = reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull));
-          const u32x4a4 a = p4[0], b = p4[1], d = p4[2];
-          w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y;
-          w[6] = b.z; w[7] = b.w; w[8] = d.x; w[9] = d.y; w[10] = d.z; w[11] = d.w;
-        }
-#pragma unroll
-        for (uint32_t e = 0; e < 16; ++e) {
-          // 16-bit entry e is halfword e + odd of the aligned dwords (compile-time indices: e is unrolled)
-          const uint32_t x0 = (e & 1u) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xFFFFu);
-          const uint32_t x1 = ((e + 1) & 1u) ? (w[(e + 1) >> 1] >> 16) : (w[(e + 1) >> 1] & 0xFFFFu);
-          const uint32_t x = odd ? x1 : x0;
-          v[u][e] = small && e < c[u].count ? x : 0u;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        if (si[u] < 0) continue;
-        if (c[u].kind == 0 && c[u].count <= 16) {
-          uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c[u].key % (uint32_t)G);
-#pragma unroll
-          for (uint32_t e = 0; e < 16; ++e)
-            if (e < c[u].count) atomicOr(&lb[v[u][e] >> 5], 1u << (v[u][e] & 31));
-        } else {
-          bigq[atomicAdd(&nbig, 1)] = si[u];
-        }
-      }
-      __syncthreads();
-      const int nb = nbig;
-      for (int qi = wave; qi < nb; qi += kBlock / 64) {
-        const RoaringContainer c = expand_desc(J, bigq[qi]);
-        const uint8_t* p = J.inv + c.offset;
-        uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c.key % (uint32_t)G);
-        if (c.kind == 1) {
-          for (int i = lane; i < 1024; i += 64) {
-            const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
-            if (w) {
-              atomicOr(&lb[2 * i], (uint32_t)w);
-              atomicOr(&lb[2 * i + 1], (uint32_t)(w >> 32));
-            }
-          }
-        } else if (c.kind == 0) {
-          const uint16_t* p16 = reinterpret_cast<const uint16_t*>(p);
-          for (uint32_t e = lane; e < c.count; e += 64) {
-            const uint32_t d = p16[e];
-            atomicOr(&lb[d >> 5], 1u << (d & 31));
-          }
-        } else {
-          for (uint32_t r = 0; r < c.count; ++r) {
-            const uint8_t* q = p + 2 + 4 * r;
-            const uint32_t s0 = q[0] | (q[1] << 8);
-            const uint32_t e0 = s0 + (q[2] | (q[3] << 8));  // inclusive, < 65536
-            const uint32_t w0 = s0 >> 5, w1 = e0 >> 5;
-            for (uint32_t w = w0 + lane; w <= w1; w += 64) {
-              uint32_t m = ~0u;
-              if (w == w0) m &= ~0u << (s0 & 31);
-              if (w == w1) m &= ~0u >> (31 - (e0 & 31));
-              atomicOr(&lb[w], m);
-            }
-          }
-        }
-      }
-      __syncthreads();
-      if (tid == 0) nbig = 0;
-      __syncthreads();
-    }
-    // write the chunk (docs >= num_docs are never set: bitmaps hold only the segment's docIds)
+    expand_item<G>(J, k, lbits, bigq, &nbig);
+    // write the group (docs >= num_docs are never set: bitmaps hold only the segment's docIds)
     const int64_t w_begin = (int64_t)k * 1024 * G;
     for (int i = tid; i < 1024 * G; i += kBlock) {
       const int64_t w = w_begin + i;
@@ -809,6 +820,120 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
   }
 }
 
+// Fused inverted-index select (word-level select plans whose every leaf is an inverted-index docId
+// bitset, a sorted-index docId range or a constant): a work item is a group of G chunks of one segment.
+// Per clause, the block expands each bitset leaf's containers for the group into LDS and ORs the words
+// into per-thread clause words (4G 64-bit words per thread), then ANDs the clause into the match words;
+// the group's matching docIds go straight to the selection vector (one reservation per item, padded to a
+// quad: an item is one segment). No dense bitset is written to or read back from HBM, and the expansion
+// and the word-level select are one launch.
+template <int G>
+__global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob* jobs, const FusedSelSeg* fs, int32_t nfs,
+                                                               int64_t total_items, const DevSegment* segs,
+                                                               int32_t nleaves, int32_t nclauses,
+                                                               unsigned long long* sel_entries, unsigned long long* sel_count,
+                                                               int64_t sel_cap, unsigned long long* matched_out) {
+  __shared__ uint32_t lbits[2048 * G];
+  __shared__ int32_t bigq[kBlock * kExpandPer];
+  __shared__ int32_t nbig;
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ unsigned long long sbase;
+  constexpr int NW = 4 * G;  // 64-bit words per thread: word tid + 256 i of the group's 1024 G
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    int lo = 0, hi = nfs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (fs[mid].item_begin <= item) lo = mid; else hi = mid - 1;
+    }
+    const FusedSelSeg& F = fs[lo];
+    const int32_t k = (int32_t)(item - F.item_begin);
+    const DevSegment& sg = segs[F.seg];
+    const int64_t w0 = (int64_t)k * 1024 * G;  // the group's first 64-doc word in the segment
+    uint64_t mt[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int64_t d0 = (w0 + tid + 256 * i) * 64;
+      mt[i] = d0 >= sg.num_docs ? 0ull : sg.num_docs - d0 >= 64 ? ~0ull : ((1ull << (sg.num_docs - d0)) - 1ull);
+    }
+    for (int c = 0; c < nclauses; ++c) {
+      uint64_t ac[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) ac[i] = 0ull;
+      for (int j = 0; j < nleaves; ++j) {
+        const DevLeaf& L = sg.leaves[j];
+        if (L.clause != c) continue;
+        uint64_t x[NW];
+        if (L.kind == LEAF_DOC_BITSET && F.job[j] >= 0) {
+          for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
+          if (tid == 0) nbig = 0;
+          __syncthreads();
+          expand_item<G>(jobs[F.job[j]], k, lbits, bigq, &nbig);
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < NW; ++i) {
+            const int w = tid + 256 * i;
+            x[i] = (uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32);
+          }
+          __syncthreads();  // the region is refilled by the next leaf
+        } else if (L.kind == LEAF_DOC_RANGE) {
+#pragma unroll
+          for (int i = 0; i < NW; ++i) {
+            const int64_t d0 = (w0 + tid + 256 * i) * 64;
+            const int64_t a = max(L.lo_i - d0, (int64_t)0), b = min(L.hi_i - d0, (int64_t)63);
+            x[i] = a > b ? 0ull : ((~0ull >> (63 - (b - a))) << a);
+          }
+        } else {  // LEAF_CONST
+#pragma unroll
+          for (int i = 0; i < NW; ++i) x[i] = L.lo_i ? ~0ull : 0ull;
+        }
+#pragma unroll
+        for (int i = 0; i < NW; ++i) ac[i] |= L.negate ? ~x[i] : x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NW; ++i) mt[i] &= ac[i];
+    }
+    // block prefix of the match counts, one vector reservation per item
+    uint32_t cnt = 0u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) cnt += (uint32_t)__popcll(mt[i]);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+    for (int w = 0; w < kBlock / 64; ++w) { if (w < wave) before += wsum[w]; total += wsum[w]; }
+    const uint32_t padded = (total + 3u) & ~3u;
+    if (tid == 0) {
+      unsigned long long b = ~0ull;
+      if (total) {
+        b = atomicAdd(sel_count, (unsigned long long)padded);
+        if (b + padded > (unsigned long long)sel_cap) { atomicAdd(sel_count + 1, 1ull); b = ~0ull; }
+        atomicAdd(matched_out, (unsigned long long)total);
+      }
+      sbase = b;
+    }
+    __syncthreads();
+    const unsigned long long base = sbase;
+    if (total && base != ~0ull) {
+      const unsigned long long tag = (unsigned long long)(uint32_t)F.seg << 32;
+      unsigned long long p = base + before + incl - cnt;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        uint64_t m = mt[i];
+        const int64_t d0 = (w0 + tid + 256 * i) * 64;
+        while (m) {
+          const int bt = __builtin_ctzll(m);
+          m &= m - 1ull;
+          sel_entries[p++] = tag | (unsigned long long)(uint32_t)(d0 + bt);
+        }
+      }
+      if (tid < (int)(padded - total)) sel_entries[base + total + tid] = tag | 0xFFFFFFFFull;
+    }
+    __syncthreads();  // wsum / sbase reused by the next item
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // launchers (called from host.cpp)
@@ -1249,6 +1374,23 @@ int expand_group() {
     return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }();
   return g;
+}
+
+hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t nfs, int64_t total_items, const void* d_segs,
+                                 int32_t nleaves, int32_t nclauses, unsigned long long* sel_entries,
+                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, hipStream_t st) {
+  if (nfs <= 0 || total_items <= 0) return hipSuccess;
+  const ExpandJob* jobs = reinterpret_cast<const ExpandJob*>(d_jobs);
+  const FusedSelSeg* fs = reinterpret_cast<const FusedSelSeg*>(d_fs);
+  const DevSegment* segs = reinterpret_cast<const DevSegment*>(d_segs);
+  const int64_t blocks = std::min<int64_t>(total_items, 16384);
+  switch (expand_group()) {
+    case 8: hipLaunchKernelGGL(roaring_select_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+    case 4: hipLaunchKernelGGL(roaring_select_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+    case 2: hipLaunchKernelGGL(roaring_select_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+    default: hipLaunchKernelGGL(roaring_select_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st) {
