@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
       for (int j = 0; j < nleaves; ++j) {
         const DevLeaf& L = sg.leaves[j];
         if (L.clause != c) continue;
-        uint64_t x[NW];
+        const uint64_t neg = L.negate ? ~0ull : 0ull;  // x ^ neg: the leaf's words, negated or not
         if (L.kind == LEAF_DOC_BITSET && F.job[j] >= 0) {
           for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
           if (tid == 0) nbig = 0;
@@ -873,7 +873,7 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
 #pragma unroll
           for (int i = 0; i < NW; ++i) {
             const int w = tid + 256 * i;
-            x[i] = (uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32);
+            ac[i] |= ((uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32)) ^ neg;
           }
           __syncthreads();  // the region is refilled by the next leaf
         } else if (L.kind == LEAF_DOC_RANGE) {
@@ -881,14 +881,12 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
           for (int i = 0; i < NW; ++i) {
             const int64_t d0 = (w0 + tid + 256 * i) * 64;
             const int64_t a = max(L.lo_i - d0, (int64_t)0), b = min(L.hi_i - d0, (int64_t)63);
-            x[i] = a > b ? 0ull : ((~0ull >> (63 - (b - a))) << a);
+            ac[i] |= (a > b ? 0ull : ((~0ull >> (63 - (b - a))) << a)) ^ neg;
           }
         } else {  // LEAF_CONST
 #pragma unroll
-          for (int i = 0; i < NW; ++i) x[i] = L.lo_i ? ~0ull : 0ull;
+          for (int i = 0; i < NW; ++i) ac[i] |= (L.lo_i ? ~0ull : 0ull) ^ neg;
         }
-#pragma unroll
-        for (int i = 0; i < NW; ++i) ac[i] |= L.negate ? ~x[i] : x[i];
       }
 #pragma unroll
       for (int i = 0; i < NW; ++i) mt[i] &= ac[i];
@@ -1384,7 +1382,7 @@ hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t n
   const FusedSelSeg* fs = reinterpret_cast<const FusedSelSeg*>(d_fs);
   const DevSegment* segs = reinterpret_cast<const DevSegment*>(d_segs);
   const int64_t blocks = std::min<int64_t>(total_items, 16384);
-  switch (expand_group()) {
+  switch (expand_group()) {  // the jobs' container grouping
     case 8: hipLaunchKernelGGL(roaring_select_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
     case 4: hipLaunchKernelGGL(roaring_select_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
     case 2: hipLaunchKernelGGL(roaring_select_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;

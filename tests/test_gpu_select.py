@@ -110,7 +110,7 @@ WORD_QUERIES = [
 ]
 
 
-@pytest.mark.parametrize("fused", [None, "0"], ids=["fused", "expand+wselect"])
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused", "expand+wselect"])
 @pytest.mark.parametrize("qi", range(len(WORD_QUERIES)))
 def test_word_select_vs_oracle(engine, data, monkeypatch, qi, fused):
     """Filters that read no column (inverted-index bitsets, sorted-index docId ranges, constants) select
@@ -118,10 +118,7 @@ def test_word_select_vs_oracle(engine, data, monkeypatch, qi, fused):
     fused with the roaring expansion (roaring_select_kernel, the default) and as expansion + word select."""
     monkeypatch.setenv("PINOT_AMD_SELECT", "always")
     monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
-    if fused is None:
-        monkeypatch.delenv("PINOT_AMD_FUSED_INV_SELECT", raising=False)
-    else:
-        monkeypatch.setenv("PINOT_AMD_FUSED_INV_SELECT", fused)
+    monkeypatch.setenv("PINOT_AMD_FUSED_INV_SELECT", fused)
     bufs, segs = data
     q = WORD_QUERIES[qi]
     res = engine.ServerQueryExecutor().execute(q, segs)
