@@ -822,7 +822,8 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
 // Fused inverted-index select (word-level select plans whose every leaf is a non-negated inverted-index
 // docId bitset, a sorted-index docId range or a constant): a work item is a group of G chunks of one
 // segment. Per clause, the block expands the clause's bitset leaves for the group into one LDS region
-// (containers OR in) and ANDs the clause into per-thread match words (4G 64-bit words per thread);
+// (containers OR in) and ANDs the clause into per-thread match words (4G 64-bit words per thread; 4
+// containers per lane and round as in the expansion: 2 measured 30 % slower at 0.01 %);
 // the group's matching docIds go straight to the selection vector (one reservation per item, padded to a
 // quad: an item is one segment). No dense bitset is written to or read back from HBM, and the expansion
 // and the word-level select are one launch.
@@ -866,7 +867,7 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
       for (int j = 0; j < nleaves; ++j) {
         const DevLeaf& L = sg.leaves[j];
         if (L.clause != c || L.kind != LEAF_DOC_BITSET || F.job[j] < 0) continue;
-        expand_item<G, 2>(jobs[F.job[j]], k, lbits, bigq, &nbig);
+        expand_item<G>(jobs[F.job[j]], k, lbits, bigq, &nbig);
         any = true;
       }
       __syncthreads();
