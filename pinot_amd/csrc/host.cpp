@@ -2769,7 +2769,6 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         for (int j = 0; j < kMaxLeaves; ++j) f.job[j] = -1;
         for (size_t j = 0; j < order.size(); ++j) {
           if (ls[k].leaves[j].kind != LEAF_DOC_BITSET) continue;
-          ok &= !ls[k].leaves[j].negate;  // a negated bitset leaf cannot OR into the clause's region
           for (size_t ii = 0; ii < r->inv_leaves.size(); ++ii)
             if (r->inv_leaves[ii].bitset->p == (const void*)ls[k].leaves[j].bits) f.job[j] = (int32_t)ii;
           ok &= f.job[j] >= 0 && r->inv_leaves[f.job[j]].nchunks >= f.nitems;

@@ -819,11 +819,10 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
   }
 }
 
-// Fused inverted-index select (word-level select plans whose every leaf is a non-negated inverted-index
-// docId bitset, a sorted-index docId range or a constant): a work item is a group of G chunks of one
-// segment. Per clause, the block expands the clause's bitset leaves for the group into one LDS region
-// (containers OR in) and ANDs the clause into per-thread match words (4G 64-bit words per thread; 4
-// containers per lane and round as in the expansion: 2 measured 30 % slower at 0.01 %);
+// Fused inverted-index select (word-level select plans whose every leaf is an inverted-index docId
+// bitset, a sorted-index docId range or a constant): a work item is a group of G chunks of one segment.
+// Per clause, the block expands each bitset leaf's containers for the group into LDS and ORs the words
+// into per-thread clause words (4G 64-bit words per thread), then ANDs the clause into the match words;
 // the group's matching docIds go straight to the selection vector (one reservation per item, padded to a
 // quad: an item is one segment). No dense bitset is written to or read back from HBM, and the expansion
 // and the word-level select are one launch.
@@ -856,40 +855,42 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
       const int64_t d0 = (w0 + tid + 256 * i) * 64;
       mt[i] = d0 >= sg.num_docs ? 0ull : sg.num_docs - d0 >= 64 ? ~0ull : ((1ull << (sg.num_docs - d0)) - 1ull);
     }
-    // per clause: its (non-negated) bitset leaves expanded together into the LDS region (the expansion ORs),
-    // then per word the clause's docId ranges / constants ORed in and the clause ANDed into the match words
-    // (only the match words stay live across the expansion: occupancy)
     for (int c = 0; c < nclauses; ++c) {
-      for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
-      if (tid == 0) nbig = 0;
-      __syncthreads();
-      bool any = false;
+      uint64_t ac[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) ac[i] = 0ull;
       for (int j = 0; j < nleaves; ++j) {
         const DevLeaf& L = sg.leaves[j];
-        if (L.clause != c || L.kind != LEAF_DOC_BITSET || F.job[j] < 0) continue;
-        expand_item<G>(jobs[F.job[j]], k, lbits, bigq, &nbig);
-        any = true;
-      }
-      __syncthreads();
+        if (L.clause != c) continue;
+        uint64_t x[NW];
+        if (L.kind == LEAF_DOC_BITSET && F.job[j] >= 0) {
+          for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
+          if (tid == 0) nbig = 0;
+          __syncthreads();
+          expand_item<G>(jobs[F.job[j]], k, lbits, bigq, &nbig);
+          __syncthreads();
 #pragma unroll
-      for (int i = 0; i < NW; ++i) {
-        const int w = tid + 256 * i;
-        uint64_t a = any ? ((uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32)) : 0ull;
-        const int64_t d0 = (w0 + w) * 64;
-        for (int j = 0; j < nleaves; ++j) {
-          const DevLeaf& L = sg.leaves[j];
-          if (L.clause != c) continue;
-          const uint64_t neg = L.negate ? ~0ull : 0ull;
-          if (L.kind == LEAF_DOC_RANGE) {
-            const int64_t lo = max(L.lo_i - d0, (int64_t)0), hi = min(L.hi_i - d0, (int64_t)63);
-            a |= (lo > hi ? 0ull : ((~0ull >> (63 - (hi - lo))) << lo)) ^ neg;
-          } else if (L.kind == LEAF_CONST) {
-            a |= (L.lo_i ? ~0ull : 0ull) ^ neg;
+          for (int i = 0; i < NW; ++i) {
+            const int w = tid + 256 * i;
+            x[i] = (uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32);
           }
+          __syncthreads();  // the region is refilled by the next leaf
+        } else if (L.kind == LEAF_DOC_RANGE) {
+#pragma unroll
+          for (int i = 0; i < NW; ++i) {
+            const int64_t d0 = (w0 + tid + 256 * i) * 64;
+            const int64_t a = max(L.lo_i - d0, (int64_t)0), b = min(L.hi_i - d0, (int64_t)63);
+            x[i] = a > b ? 0ull : ((~0ull >> (63 - (b - a))) << a);
+          }
+        } else {  // LEAF_CONST
+#pragma unroll
+          for (int i = 0; i < NW; ++i) x[i] = L.lo_i ? ~0ull : 0ull;
         }
-        mt[i] &= a;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) ac[i] |= L.negate ? ~x[i] : x[i];
       }
-      __syncthreads();  // the region is refilled by the next clause
+#pragma unroll
+      for (int i = 0; i < NW; ++i) mt[i] &= ac[i];
     }
     // block prefix of the match counts, one vector reservation per item
     uint32_t cnt = 0u;
