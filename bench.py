@@ -327,13 +327,16 @@ def main():
         # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
         # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
         traffic, traffic_src = None, None
-        pmc = os.path.join(ROOT, "profiles", "r02", "pmc_index.json")
-        if os.path.exists(pmc) and args.workload == "scan" and args.query_index is None:
-            d = json.load(open(pmc)).get("scan")
-            if d and d["query"] == query:
-                traffic = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows_per_rank
-                traffic_src = ("profiles/r02/pmc_index.json (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE per execution "
-                               "of this query over 40 segments, scaled per row; profiles/profile_r02.sh)")
+        for rnd in ("r03", "r02"):  # the latest committed pass of this exact query
+            pmc = os.path.join(ROOT, "profiles", rnd, "pmc_index.json")
+            if traffic is None and os.path.exists(pmc):
+                for key, d in json.load(open(pmc)).items():
+                    if d.get("query") == query and d.get("rows"):
+                        traffic = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows_per_rank
+                        traffic_src = (f"profiles/{rnd}/pmc_index.json[{key}] (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE "
+                                       f"per execution of this query over {d['rows']:.0f} rows, scaled per row; "
+                                       f"profiles/profile_{rnd}.sh)")
+                        break
 
         if rank == 0:
             cpu = None
