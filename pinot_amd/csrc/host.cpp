@@ -72,7 +72,8 @@ hipError_t launch_bitset_compact(const uint64_t* bits, int64_t num_docs, const i
 hipError_t launch_expand_jobs(const void* d_jobs, int32_t njobs, int64_t total_items, hipStream_t st);
 hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t nfs, int64_t total_items, const void* d_segs,
                                  int32_t nleaves, int32_t nclauses, unsigned long long* sel_entries,
-                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, hipStream_t st);
+                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, int clause,
+                                 hipStream_t st);
 hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int group, unsigned long long* out,
                            hipStream_t st);
 int expand_group();
@@ -1141,6 +1142,7 @@ struct Launch {
   bool fused = false;
   DevBuf d_fused;  // FusedSelSeg per segment of the launch
   int32_t nfused = 0, fused_leaves = 0, fused_clauses = 0;
+  bool fused_clause = false;  // roaring_select_clause_kernel (no negated bitset leaf)
   int64_t fused_items = 0;
   size_t shmem_sets = 0;  // LDS dictId sets of the scan / select pass (JitLeaf::lds_words)
   int gather_grid = 1, gather_threads = 256;
@@ -1662,7 +1664,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
     if (L.fused)
       HIP_OK(launch_roaring_select(r->d_expand_jobs.p, L.d_fused.p, L.nfused, L.fused_items, L.d_segs.p,
                                    L.fused_leaves, L.fused_clauses, L.q.sel_entries, L.q.sel_count, L.q.sel_cap,
-                                   matched, st));
+                                   matched, L.fused_clause ? 1 : 0, st));
     else
       HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, (unsigned)L.shmem_sets, st, args, nullptr));
     if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
@@ -2758,7 +2760,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const int G = expand_group();
       std::vector<FusedSelSeg> fv(ls.size());
       int64_t items = 0;
-      bool ok = true;
+      bool ok = true, neg_bits = false;
       for (size_t k = 0; k < ls.size(); ++k) {
         FusedSelSeg& f = fv[k];
         memset(&f, 0, sizeof(f));
@@ -2772,6 +2774,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           for (size_t ii = 0; ii < r->inv_leaves.size(); ++ii)
             if (r->inv_leaves[ii].bitset->p == (const void*)ls[k].leaves[j].bits) f.job[j] = (int32_t)ii;
           ok &= f.job[j] >= 0 && r->inv_leaves[f.job[j]].nchunks >= f.nitems;
+          neg_bits |= ls[k].leaves[j].negate != 0;
         }
         items += f.nitems;
       }
@@ -2781,6 +2784,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.nfused = (int32_t)fv.size();
         L.fused_items = items;
         L.fused_leaves = (int32_t)order.size();
+        L.fused_clause = !neg_bits && env_is("PINOT_AMD_FUSED_VARIANT", "clause");
         L.fused_clauses = base.nclauses;
       }
     }

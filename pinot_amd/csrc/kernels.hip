@@ -934,6 +934,123 @@ __global__ void __launch_bounds__(kBlock) roaring_select_kernel(const ExpandJob*
   }
 }
 
+// The same selection with a clause's non-negated bitset leaves expanded together into the LDS region (the
+// expansion ORs) and only the match words live across the expansion (fewer registers: more waves). The host
+// takes it for filters without negated bitset leaves when PINOT_AMD_FUSED_VARIANT=clause.
+template <int G>
+__global__ void __launch_bounds__(kBlock) roaring_select_clause_kernel(const ExpandJob* jobs, const FusedSelSeg* fs,
+                                                                      int32_t nfs, int64_t total_items,
+                                                                      const DevSegment* segs, int32_t nleaves,
+                                                                      int32_t nclauses, unsigned long long* sel_entries,
+                                                                      unsigned long long* sel_count, int64_t sel_cap,
+                                                                      unsigned long long* matched_out) {
+  __shared__ uint32_t lbits[2048 * G];
+  __shared__ int32_t bigq[kBlock * kExpandPer];
+  __shared__ int32_t nbig;
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ unsigned long long sbase;
+  constexpr int NW = 4 * G;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    int lo = 0, hi = nfs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (fs[mid].item_begin <= item) lo = mid; else hi = mid - 1;
+    }
+    const FusedSelSeg& F = fs[lo];
+    const int32_t k = (int32_t)(item - F.item_begin);
+    const DevSegment& sg = segs[F.seg];
+    const int64_t w0 = (int64_t)k * 1024 * G;
+    uint64_t mt[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int64_t d0 = (w0 + tid + 256 * i) * 64;
+      mt[i] = d0 >= sg.num_docs ? 0ull : sg.num_docs - d0 >= 64 ? ~0ull : ((1ull << (sg.num_docs - d0)) - 1ull);
+    }
+    for (int c = 0; c < nclauses; ++c) {
+      for (int i = tid; i < 2048 * G; i += kBlock) lbits[i] = 0u;
+      if (tid == 0) nbig = 0;
+      __syncthreads();
+      bool any = false, other = false;
+      for (int j = 0; j < nleaves; ++j) {
+        const DevLeaf& L = sg.leaves[j];
+        if (L.clause != c) continue;
+        if (L.kind == LEAF_DOC_BITSET && F.job[j] >= 0) {
+          expand_item<G>(jobs[F.job[j]], k, lbits, bigq, &nbig);
+          any = true;
+        } else {
+          other = true;
+        }
+      }
+      __syncthreads();
+      uint64_t a[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const int w = tid + 256 * i;
+        a[i] = any ? ((uint64_t)lbits[2 * w] | ((uint64_t)lbits[2 * w + 1] << 32)) : 0ull;
+      }
+      if (other)
+        for (int j = 0; j < nleaves; ++j) {
+          const DevLeaf& L = sg.leaves[j];
+          if (L.clause != c || (L.kind == LEAF_DOC_BITSET && F.job[j] >= 0)) continue;
+          const uint64_t neg = L.negate ? ~0ull : 0ull;
+          if (L.kind == LEAF_DOC_RANGE) {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+              const int64_t d0 = (w0 + tid + 256 * i) * 64;
+              const int64_t x0 = max(L.lo_i - d0, (int64_t)0), x1 = min(L.hi_i - d0, (int64_t)63);
+              a[i] |= (x0 > x1 ? 0ull : ((~0ull >> (63 - (x1 - x0))) << x0)) ^ neg;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) a[i] |= (L.lo_i ? ~0ull : 0ull) ^ neg;
+          }
+        }
+#pragma unroll
+      for (int i = 0; i < NW; ++i) mt[i] &= a[i];
+      __syncthreads();  // the region is refilled by the next clause
+    }
+    uint32_t cnt = 0u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) cnt += (uint32_t)__popcll(mt[i]);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+    for (int w = 0; w < kBlock / 64; ++w) { if (w < wave) before += wsum[w]; total += wsum[w]; }
+    const uint32_t padded = (total + 3u) & ~3u;
+    if (tid == 0) {
+      unsigned long long b = ~0ull;
+      if (total) {
+        b = atomicAdd(sel_count, (unsigned long long)padded);
+        if (b + padded > (unsigned long long)sel_cap) { atomicAdd(sel_count + 1, 1ull); b = ~0ull; }
+        atomicAdd(matched_out, (unsigned long long)total);
+      }
+      sbase = b;
+    }
+    __syncthreads();
+    const unsigned long long base = sbase;
+    if (total && base != ~0ull) {
+      const unsigned long long tag = (unsigned long long)(uint32_t)F.seg << 32;
+      unsigned long long p = base + before + incl - cnt;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        uint64_t m = mt[i];
+        const int64_t d0 = (w0 + tid + 256 * i) * 64;
+        while (m) {
+          const int bt = __builtin_ctzll(m);
+          m &= m - 1ull;
+          sel_entries[p++] = tag | (unsigned long long)(uint32_t)(d0 + bt);
+        }
+      }
+      if (tid < (int)(padded - total)) sel_entries[base + total + tid] = tag | 0xFFFFFFFFull;
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launchers (called from host.cpp)
 // ------------------------------------------------------------------------------------------------
@@ -1377,12 +1494,22 @@ int expand_group() {
 
 hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t nfs, int64_t total_items, const void* d_segs,
                                  int32_t nleaves, int32_t nclauses, unsigned long long* sel_entries,
-                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, hipStream_t st) {
+                                 unsigned long long* sel_count, int64_t sel_cap, unsigned long long* matched_out, int clause,
+                                 hipStream_t st) {
   if (nfs <= 0 || total_items <= 0) return hipSuccess;
   const ExpandJob* jobs = reinterpret_cast<const ExpandJob*>(d_jobs);
   const FusedSelSeg* fs = reinterpret_cast<const FusedSelSeg*>(d_fs);
   const DevSegment* segs = reinterpret_cast<const DevSegment*>(d_segs);
   const int64_t blocks = std::min<int64_t>(total_items, 16384);
+  if (clause) {
+    switch (expand_group()) {
+      case 8: hipLaunchKernelGGL(roaring_select_clause_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+      case 4: hipLaunchKernelGGL(roaring_select_clause_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+      case 2: hipLaunchKernelGGL(roaring_select_clause_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+      default: hipLaunchKernelGGL(roaring_select_clause_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
+    }
+    return hipGetLastError();
+  }
   switch (expand_group()) {  // the jobs' container grouping
     case 8: hipLaunchKernelGGL(roaring_select_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
     case 4: hipLaunchKernelGGL(roaring_select_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), 0, st, jobs, fs, nfs, total_items, segs, nleaves, nclauses, sel_entries, sel_count, sel_cap, matched_out); break;
