@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 out=gpurun_out/sweep.txt
 : > $out
 for kv in ${SWEEP:-none}; do
-  if [ "$kv" = none ]; then envset=""; else envset="$kv"; fi
+  if [ "$kv" = none ]; then envset=""; else envset="${kv//,/ }"; fi  # A=1,B=2: several variables
   env $envset timeout -k 10 300 python bench.py $ARGS --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/sweep_one.json 2> gpurun_out/sweep_one.err || { echo "$kv FAILED"; tail -5 gpurun_out/sweep_one.err; exit 1; }
   python -c "
 import json
