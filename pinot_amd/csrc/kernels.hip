@@ -723,8 +723,14 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, int32_t k, uint3
       uint32_t w[12];
       const uint32_t odd = (uint32_t)(c[u].offset >> 1) & 1u;  // entry 0 in the dword's high half
       if (small) {
+        // only the 16-byte pieces the entries reach (halfwords odd .. odd + count - 1): with a few docs per
+        // container (selective IN lists) one piece, so the neighbouring containers' pieces share lines
         const u32x4a4* p4 = reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull));
-        const u32x4a4 a = p4[0], b = p4[1], d = p4[2];
+        const uint32_t reach = odd + c[u].count;
+        const u32x4a4 a = p4[0];
+        u32x4a4 b = (u32x4a4)(0u), d = (u32x4a4)(0u);
+        if (reach > 8u) b = p4[1];
+        if (reach > 16u) d = p4[2];
         w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y;
         w[6] = b.z; w[7] = b.w; w[8] = d.x; w[9] = d.y; w[10] = d.z; w[11] = d.w;
       }
