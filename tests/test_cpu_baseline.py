@@ -30,3 +30,23 @@ def test_cpu_plan_inverted_or():
     exp, _ = oracle.execute(q, [seg])
     run = oracle.cpu_plan(q, seg)
     assert exp > 0 and run() == exp and run() == exp
+
+
+@pytest.mark.parametrize("info,want", [
+    ("jit", "pinot_scan_jit"),
+    ("jit-select", "pinot_select+pinot_gather"),
+    ("jit-wselect", "pinot_select(word-level)+pinot_gather"),
+    ("jit-fwselect", "roaring_select_kernel"),
+    ("jit-partitioned+admit-seq", "pinot_admit_seq"),
+    ("jit-partitioned+admit", "pinot_first_doc"),
+    ("jit-hash-trim", "hash_merge_kernel"),
+    ("jit x3", "(3 shape launches)"),
+])
+def test_bench_kernel_labels(info, want):
+    """bench.py names the kernels a plan ran from its kernel_info (round-2 advisor: mislabelled lines)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert want in bench.plan_kernels(info), bench.plan_kernels(info)
