@@ -9,19 +9,23 @@ N > 1, the RCCL all-reduce of the dense group tables. Segments are independent, 
 fixed as N grows (weak scaling).
 
 Other workloads (one JSON line per query; not the driver's headline line):
+  --workload readme     configs[0]: the README's AdAnalytics query on one 10M-row segment (CPU baseline on
+                        one thread: one segment is one Pinot worker's task)
   --workload highcard   configs[3]: GROUP BY two 1000-value dimensions (1M groups), numGroupsLimit raised
                         above the key space (every group kept): partitioned plan
   --workload highcard-default  configs[3]'s query at Pinot's default numGroupsLimit (100000 < 1M groups
-                        per segment): exact first-seen trimming per segment, hash-table plan
+                        per segment): exact first-seen trimming per segment (sequential admission pass,
+                        then the partitioned plan over the admitted docs)
   --workload inverted   configs[2]: inverted-index IN filters, AND/OR over 3 columns, selectivity sweep
   --workload ssb        configs[4]: SSB SF100 denormalized lineorder, Q1.1-Q4.3
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload scan|highcard|inverted]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload readme|scan|highcard|highcard-default|inverted|ssb]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -42,6 +46,9 @@ def workloads():
     """name -> (segment generator, [queries], algorithmic HBM bytes per row, description, distinct segments)."""
     from pinot_amd import datagen, ssb
     return {
+        "readme": (datagen.ad_segment, [datagen.README_QUERY], None,
+                   "configs[0]: one 10M-row immutable segment of the AdAnalytics table, the reference README's "
+                   "example query (8-day range AND IN filter, SUM clicks/impressions GROUP BY daysSinceEpoch)", None),
         "scan": (datagen.ad_segment, [datagen.BENCH_QUERY], datagen.BENCH_BYTES_PER_ROW,
                  "configs[1]: 1B rows in 100 segments per GPU, fixed-bit dict + raw INT/LONG/DOUBLE columns; "
                  "filter+group-by query", None),
@@ -126,10 +133,37 @@ def plan_kernels(info: str) -> str:
     return k
 
 
+def query_sha1(query: str) -> str:
+    return hashlib.sha1(query.encode()).hexdigest()
+
+
+def committed_traffic(query: str, kernel_info: str, rows: int):
+    """HBM traffic per execution from the latest committed rocprofv3 PMC pass of this exact query (matched by
+    the SHA-1 of its full text) on this exact device plan (pinot_amd_result_kernel_info): FETCH_SIZE x 2 (the
+    gfx950 correction of MI355X_MICROARCH.md) + WRITE_SIZE, per row of the profiled run, scaled to `rows`.
+    A record of another plan (a planner change since the pass) is not used: traffic is then None."""
+    sha = query_sha1(query)
+    for rnd in ("r04", "r03"):
+        pmc = os.path.join(ROOT, "profiles", rnd, "pmc_index.json")
+        if not os.path.exists(pmc):
+            continue
+        for key, d in json.load(open(pmc)).items():
+            if not d.get("rows") or (d.get("query_sha1") or (query_sha1(d["query"]) if "query" in d else None)) != sha:
+                continue
+            if d.get("scan_kernel") != kernel_info:  # unrecorded plan (round 3 records): not evidence
+                continue
+            t = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows
+            src = (f"profiles/{rnd}/pmc_index.json[{key}] (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE per execution of "
+                   f"this query on plan {d.get('scan_kernel', '?')} over {d['rows']:.0f} rows, commit "
+                   f"{d.get('commit', '?')}, scaled per row; profiles/profile_{rnd}.sh)")
+            return t, src
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="scan", choices=["scan", "highcard", "highcard-default", "inverted", "ssb"])
+    ap.add_argument("--workload", default="scan", choices=["readme", "scan", "highcard", "highcard-default", "inverted", "ssb"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default 100; ssb: 60 = SF100)")
@@ -164,7 +198,9 @@ def main():
     if args.query_index is not None:
         queries = [queries[args.query_index]]
     if args.segments is None:
-        args.segments = 60 if args.workload == "ssb" else 100
+        args.segments = {"ssb": 60, "readme": 1}.get(args.workload, 100)
+    if args.workload == "readme":  # a single segment: one Pinot worker thread
+        args.cpu_threads = min(args.cpu_threads, args.segments)
     if args.cpu_seconds is None:
         args.cpu_seconds = 12.0 if len(queries) == 1 else 4.0
     cpu_cache: dict = {}
@@ -225,13 +261,16 @@ def main():
         t_f = time.perf_counter()
         arrays = res2.fetch_arrays() if hasattr(res2, "fetch_arrays") else None
         t_g = time.perf_counter()
-        res2.groups()
+        if arrays is not None:  # Python conversion of the arrays already fetched (no second fetch)
+            res2.groups(arrays=arrays)
+        else:
+            res2.groups()
         t_e = time.perf_counter()
         plan_ms = (t_e - t_c) * 1e3
         host_ms = {  # the cached-plan query's host time: library planning + first execution, library fetch
             "execute_ms": (t_f - t_c) * 1e3,  # (device compaction + copy of the groups), Python conversion
             "fetch_ms": (t_g - t_f) * 1e3 if arrays is not None else None,
-            "python_groups_ms": (t_e - t_g) * 1e3 - ((t_g - t_f) * 1e3 if arrays is not None else 0.0),
+            "python_groups_ms": (t_e - t_g) * 1e3,
             "plan_phases_ms": res2.plan_timing() if hasattr(res2, "plan_timing") else None,
         }
         del arrays
@@ -282,9 +321,13 @@ def main():
         # decoded column once at its stored width; under an inverted-index gate only the rows that
         # pass it, plus the selected bitmaps and the dense bitset written + read once
         alg_bytes = res.algorithmic_bytes()
-        if bytes_per_row is not None and abs(alg_bytes - rows_per_rank * bytes_per_row) > 1e-6 * alg_bytes:
-            log(f"warning: plan's algorithmic bytes {alg_bytes / rows_per_rank:.4f} B/row != {bytes_per_row:.4f}")
         bpr = alg_bytes / rows_per_rank
+        # the workload's own count of the query's column bytes (datagen); the roofline uses the plan's
+        # figure, and a disagreement is reported on the line, not hidden in the log
+        bpr_mismatch = None
+        if bytes_per_row is not None and abs(alg_bytes - rows_per_rank * bytes_per_row) > 1e-6 * alg_bytes:
+            bpr_mismatch = {"plan_bytes_per_row": bpr, "workload_bytes_per_row": bytes_per_row}
+            log(f"warning: plan's algorithmic bytes {bpr:.4f} B/row != {bytes_per_row:.4f}")
         achieved = alg_bytes / avg_kernel_s / 1e9
 
         groups = res.groups()
@@ -324,19 +367,7 @@ def main():
                         assert g == e, (k, a.name, g, e)
             log("[check] HIP result == oracle on a 2M-row segment")
 
-        # HBM traffic per launch from the committed rocprofv3 PMC pass of this kernel and query
-        # (FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950 correction + WRITE_SIZE), scaled per row
-        traffic, traffic_src = None, None
-        for rnd in ("r03", "r02"):  # the latest committed pass of this exact query
-            pmc = os.path.join(ROOT, "profiles", rnd, "pmc_index.json")
-            if traffic is None and os.path.exists(pmc):
-                for key, d in json.load(open(pmc)).items():
-                    if d.get("query") == query and d.get("rows"):
-                        traffic = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows_per_rank
-                        traffic_src = (f"profiles/{rnd}/pmc_index.json[{key}] (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE "
-                                       f"per execution of this query over {d['rows']:.0f} rows, scaled per row; "
-                                       f"profiles/profile_{rnd}.sh)")
-                        break
+        traffic, traffic_src = committed_traffic(query, res.kernel_info(), rows_per_rank)
 
         if rank == 0:
             cpu = None
@@ -360,6 +391,7 @@ def main():
                 "config": {
                     "workload": workload_desc,
                     "query": query if len(query) < 400 else query[:200] + " ... " + query[-120:],
+                    "query_sha1": query_sha1(query),
                     "segments_per_gpu": args.segments,
                     "rows_per_segment": args.rows,
                     "rows_per_gpu": rows_per_rank,
@@ -386,6 +418,7 @@ def main():
                     "kernel_ms_source": "mean of HIP events recorded on the plan's stream around each timed execution",
                     "library_last_kernel_ms": lib_kernel_ms,
                     "bytes_per_row": bpr,
+                    "bytes_per_row_mismatch": bpr_mismatch,
                 },
                 "cpu_baseline": cpu,
             }

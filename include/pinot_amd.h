@@ -214,6 +214,14 @@ int pinot_amd_query_set_num_groups_limit(pinot_amd_query* q, int64_t limit);
  * the server-side IndexedTable of GroupByCombineOperator; not set: every group is returned. */
 int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t min_server_group_trim_size,
                                      int64_t group_trim_threshold);
+/* Query options of the server result's size (defaults 0 / 10000): serverReturnFinalResult (with ORDER BY and
+ * no HAVING the table keeps LIMIT groups, GroupByUtils.java:134-139) and sortAggregateLimitThreshold. With
+ * ORDER BY keys = GROUP BY keys (safe trim, QueryContext.java:568-580,746-747) and LIMIT below the threshold,
+ * Pinot's sorted combine (CombinePlanNode.java:150-154) keeps the top LIMIT groups, exact; at or above it each
+ * segment keeps its top LIMIT groups (GroupByOperator.java:146-182) -- execute then returns EUNSUPPORTED when
+ * some segment could hold more than LIMIT groups (that segment-level trim is not restated). */
+int pinot_amd_query_set_server_options(pinot_amd_query* q, int32_t server_return_final_result,
+                                       int64_t sort_aggregate_limit_threshold);
 /* ORDER BY key of the server table, in order of precedence: kind 0 = group-by column `index` (value
  * order), kind 1 = aggregation `index` (final value, Double.compare); ascending != 0 for ASC. */
 int pinot_amd_query_add_order_by(pinot_amd_query* q, int32_t kind, int32_t index, int32_t ascending);
@@ -276,20 +284,26 @@ int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int
  * merged key space's ids packed <= 63 bits per word) at d_keys[g * key_words], h_num_acc accumulator
  * words per group at d_acc[g * num_acc] (the library's encoding). d_keys / d_acc NULL: only the three
  * sizes. Every rank exports the same layout once the same global key space is installed
- * (pinot_amd_query_set_group_key_values). merge_groups folds n such rows (every rank's, gathered over
- * RCCL) into one device hash table with the accumulator ops; until the next execution the result's
- * groups (num_groups / fetch / fetch_intermediate) are the merged ones. */
+ * (pinot_amd_query_set_group_key_values). merge_groups folds n such rows (a rank's share of every
+ * rank's rows, exchanged over RCCL) into one device hash table with the accumulator ops; until the next
+ * execution the result's groups (num_groups / fetch / fetch_intermediate / export_groups) are the merged
+ * ones, so a key-partitioned merge can export its merged share again. `stream` (NULL: the result's
+ * stream) is ordered after the result's own stream by the library and used for this call only. */
 int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64_t* d_acc, int64_t cap,
                                    int32_t* h_key_words, int32_t* h_num_acc, int64_t* h_num_groups, void* stream);
 int pinot_amd_result_merge_groups(pinot_amd_result* r, const uint64_t* d_keys, const uint64_t* d_acc, int64_t n,
                                   void* stream);
-/* The device plan: "jit" (fused scan), "jit-select" / "jit-wselect" (selection vector), "jit-partitioned",
- * "jit-hash", "jit-hash-trim"; " xN" when the batch ran as N shape launches. */
+/* The device plan: "jit" (fused scan), "jit-partitioned", "jit-hash", "jit-hash-trim"; then "-select" /
+ * "-wselect" / "-fwselect" for a selection-vector plan (filter on 4-doc tiles / on 64-doc bitset words /
+ * fused with the inverted-index expansion), "+admit-seq" / "+admit" for numGroupsLimit admission
+ * (sequential / first-doc), and " xN" when the batch ran as N shape launches. */
 const char* pinot_amd_result_kernel_info(pinot_amd_result* r);
 /* Algorithmic HBM bytes of the last execution (the roofline numerator): every decoded column once
  * (fixed-bit columns at their bit width, raw columns at their value width); under an inverted-index
- * gate only the rows that pass it; plus, per inverted-index leaf, the selected bitmaps' serialized
- * bytes and the dense docId bitset written and read once. */
+ * gate only the rows that pass it; selection-vector plans: the filter columns of every doc, 16 B per
+ * vector entry (written + read) and the gathered columns of the matches; plus, per inverted-index leaf,
+ * the selected bitmaps' serialized bytes and -- only when the expansion writes one -- the dense docId
+ * bitset written and read once (the fused -fwselect plan writes none). */
 int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes);
 /* Host planning time of the execute that built this result, per phase, as "phase=ms;..." (raw_keys:
  * derived dictionaries of raw GROUP BY columns; leaves: per-segment predicate resolution; keys_probe:

@@ -25,8 +25,12 @@ import dataclasses
 from pinot_amd.query import Aggregation, QueryContext, parse_sql  # the SQL front end only: no arithmetic
 from oracle_reduce import JDouble, identity_key, java_identity, merge
 from oracle_reduce import rows as reduce_rows
-from pinot_amd.segment import (DOUBLE, FLOAT, INT, LONG, STRING, ColumnBuffers, SegmentBuffers,
-                               parse_raw_fwd_header)
+
+# Segments arrive as the test fixtures' column-buffer records (name, stored_type, num_docs, has_dictionary,
+# encoding, cardinality, bits_per_element, fwd / dictionary / inverted bytes, dict_values); the oracle reads
+# their attributes only and parses every byte format itself (no product code in the checker).
+INT, LONG, FLOAT, DOUBLE, STRING = "INT", "LONG", "FLOAT", "DOUBLE", "STRING"  # FieldSpec.DataType names
+ColumnBuffers = SegmentBuffers = object  # annotations only
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libpinot_oracle.so")
@@ -260,16 +264,47 @@ def _zstd_content_size(fr: bytes) -> int:
     return v + 256 if size == 2 else v
 
 
+class _RawHeader:
+    """BaseChunkForwardIndexReader's header fields (BaseChunkForwardIndexReader.java:60-105): version,
+    chunk count, docs per chunk, entry size, then (version >= 2) total docs, ChunkCompressionType and the
+    data header start; version 1 files are SNAPPY with a 16-byte header."""
+
+    def __init__(self, buf: bytes):
+        import struct
+        self.version, self.num_chunks, self.docs_per_chunk, self.size_of_entry = struct.unpack_from(">4i", buf, 0)
+        if self.version > 1:
+            self.total_docs, self.compression, self.data_header_start = struct.unpack_from(">3i", buf, 16)
+        else:
+            self.total_docs, self.compression, self.data_header_start = -1, 1, 16
+        self.raw_data_start = self.data_header_start + self.num_chunks * (4 if self.version <= 2 else 8)
+
+
+def parse_raw_fwd_header(buf: bytes) -> _RawHeader:
+    return _RawHeader(buf)
+
+
+def _bits_per_value(max_value: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue (PinotDataBitSet.java:61-72): at least one bit."""
+    return 1 if max_value <= 1 else int(max_value).bit_length()
+
+
 def _dictionary_twin(cb: ColumnBuffers) -> ColumnBuffers:
-    """ForwardIndexHandler ENABLE_DICTIONARY restated for a raw STRING column: sorted distinct values
-    (String.compareTo order) and a fixed-bit dictId forward index."""
-    from pinot_amd.segment import build_dictionary, dictionary_bytes, num_bits_per_value, pack_fixed_bit
-    vals = np.array(var_byte_values(cb), dtype=object)
-    dvals, ids = build_dictionary(vals, STRING)
-    card = max(len(dvals), 1)
-    bits = num_bits_per_value(card - 1)
-    return ColumnBuffers(cb.name, STRING, cb.num_docs, True, False, card, bits, pack_fixed_bit(ids, bits),
-                         dictionary_bytes(dvals, STRING), None, dvals)
+    """ForwardIndexHandler ENABLE_DICTIONARY restated for a raw STRING column: the sorted distinct values
+    (SegmentDictionaryCreator; String.compareTo order = UTF-16 code units) and a fixed-bit dictId forward
+    index written by the oracle's own PinotDataBitSet.writeInt restatement (oracle_fixedbit_write)."""
+    vals = var_byte_values(cb)
+    uniq = sorted(set(vals), key=lambda v: v.encode("utf-16-be"))
+    index = {v: i for i, v in enumerate(uniq)}
+    ids = np.fromiter((index[v] for v in vals), dtype=np.int32, count=len(vals))
+    card = max(len(uniq), 1)
+    bits = _bits_per_value(card - 1)
+    packed = np.zeros((len(vals) * bits + 7) // 8 + 16, dtype=np.uint8)
+    lib().oracle_fixedbit_write(_ptr(packed), bits, 0, len(vals), _ptr(ids))
+    width = max([len(v.encode("utf-8")) for v in uniq] + [1])
+    dict_bytes = b"".join(v.encode("utf-8").ljust(width, b"\0") for v in uniq)
+    return dataclasses.replace(cb, has_dictionary=True, is_sorted=False, cardinality=card, bits_per_element=bits,
+                               fwd=packed[:(len(vals) * bits + 7) // 8].tobytes(), dictionary=dict_bytes,
+                               inverted=None, dict_values=np.array(uniq, dtype=object))
 
 
 def raw_values_region(cb: ColumnBuffers) -> np.ndarray:
@@ -302,7 +337,7 @@ class OracleSegment:
 
     def __init__(self, seg: SegmentBuffers):
         if any(c.stored_type == STRING and not c.has_dictionary for c in seg.columns.values()):
-            seg = SegmentBuffers(seg.name, seg.num_docs, {
+            seg = dataclasses.replace(seg, columns={
                 n: _dictionary_twin(c) if (c.stored_type == STRING and not c.has_dictionary) else c
                 for n, c in seg.columns.items()})
         self.seg = seg

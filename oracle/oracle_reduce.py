@@ -131,7 +131,11 @@ def server_table(qc, groups: dict) -> dict:
     IndexedTable.finish) over the combined groups: without ORDER BY the first LIMIT groups (taken in
     ascending group-key order: the key compares its last group-by column first, each column in dictionary
     order); with ORDER BY the top trimSize = max(5 * LIMIT, minServerGroupTrimSize) groups by the ORDER BY
-    on final values (ties in ascending key order), none dropped when minServerGroupTrimSize <= 0.
+    on final values (ties in ascending key order), none dropped when minServerGroupTrimSize <= 0. Two cases
+    keep LIMIT groups instead: serverReturnFinalResult without HAVING (GroupByUtils.java:134-139), and a safe
+    trim -- ORDER BY expressions = GROUP BY expressions as sets, QueryContext.java:746-747 -- with LIMIT below
+    sortAggregateLimitThreshold, where CombinePlanNode.java:150-154 picks the sorted combine whose merger keeps
+    LIMIT records (SortedGroupByCombineOperator, GroupByUtils.getSortedReduceMerger).
     Returns the kept groups (a dict in the table's order)."""
     keys = sorted(groups, key=lambda k: tuple(_value_order(v) for v in reversed(k)))
     if not qc.order_by:
@@ -149,7 +153,13 @@ def server_table(qc, groups: dict) -> dict:
             parts.append(o if asc else _Desc(o))
         return tuple(parts) + (rank[k],)
     ordered = sorted(keys, key=sort_key)
-    trim = max(5 * qc.limit, qc.min_server_group_trim_size) if qc.min_server_group_trim_size > 0 else len(ordered)
+    same_keys = all(kind == 0 for kind, _, _ in targets) and \
+        sorted({idx for _, idx, _ in targets}) == list(range(len(qc.group_by)))
+    if (same_keys and qc.limit < getattr(qc, "sort_aggregate_limit_threshold", 10_000)) or \
+            getattr(qc, "server_return_final_result", False):
+        trim = qc.limit
+    else:
+        trim = max(5 * qc.limit, qc.min_server_group_trim_size) if qc.min_server_group_trim_size > 0 else len(ordered)
     return {k: groups[k] for k in ordered[:trim]}
 
 

@@ -967,6 +967,10 @@ struct pinot_amd_query {
   struct OrderBy { int kind, index, asc; };  // kind 0: group-by column `index`, 1: aggregation `index`
   std::vector<OrderBy> order_by;
   int64_t min_trim = 5000, trim_threshold = 1000000;
+  // query options of the server's result sizing: serverReturnFinalResult (GroupByUtils.java:134-139) and
+  // sortAggregateLimitThreshold (QueryContext.shouldSortAggregateUnderSafeTrim, default 10000)
+  int server_final = 0;
+  int64_t sort_agg_threshold = 10000;
 };
 
 extern "C" {
@@ -1102,6 +1106,14 @@ int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t 
   return 0;
 }
 
+int pinot_amd_query_set_server_options(pinot_amd_query* q, int32_t server_return_final_result,
+                                       int64_t sort_aggregate_limit_threshold) {
+  if (!q || sort_aggregate_limit_threshold <= 0) return fail(PINOT_AMD_EINVAL, "set_server_options: bad arguments");
+  q->server_final = server_return_final_result ? 1 : 0;
+  q->sort_agg_threshold = sort_aggregate_limit_threshold;
+  return 0;
+}
+
 int pinot_amd_query_add_order_by(pinot_amd_query* q, int32_t kind, int32_t index, int32_t ascending) {
   if (!q || (kind != 0 && kind != 1) || index < 0) return fail(PINOT_AMD_EINVAL, "add_order_by: bad arguments");
   if (kind == 0 && index >= (int32_t)q->group_by.size())
@@ -1177,7 +1189,8 @@ struct pinot_amd_result {
     DevBuf* grp;   // chunk k's containers: sel[grp[k] .. grp[k+1])
     int32_t nsel, nchunks;
     int64_t num_docs;
-    double alg_bytes;  // selected bitmap payloads + the dense bitset written and read once
+    double alg_bytes;     // the selected bitmaps' serialized bytes (read once)
+    double bitset_bytes;  // the dense docId bitset written and read once (only when the expansion runs)
     DevBuf* psel = nullptr;  // packed descriptors in sel order (ExpandJob::psel), or none
   };
   std::vector<InvLeaf> inv_leaves;
@@ -1196,6 +1209,7 @@ struct pinot_amd_result {
   std::vector<int32_t> agg_type;
   int32_t num_group_by = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_x = nullptr;  // orders a cross-rank call's stream after the result's (call_stream)
   std::string jit_status;
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
@@ -1237,6 +1251,9 @@ struct pinot_amd_result {
   // server-level IndexedTable (pinot_amd_query_set_result_limit / add_order_by), applied at compaction
   int64_t srv_limit = -1, srv_min_trim = 5000, srv_trim_threshold = 1000000;
   std::vector<pinot_amd_query::OrderBy> srv_order;
+  int srv_final = 0;                   // serverReturnFinalResult
+  int64_t srv_sort_threshold = 10000;  // sortAggregateLimitThreshold
+  bool srv_safe = false;               // ORDER BY keys = GROUP BY keys, no HAVING (QueryContext._isUnsafeTrim false)
   bool srv_trimmed = false;
   // host planning time per phase (pinot_amd_result_plan_timing)
   std::string plan_timing;
@@ -1247,6 +1264,7 @@ struct pinot_amd_result {
   ~pinot_amd_result() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (ev_x) (void)hipEventDestroy(ev_x);
   }
 };
 
@@ -1526,7 +1544,7 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
     double sel_bytes = 0;
     for (int32_t d : ids) sel_bytes += (double)(c.inv_bytes[d + 1] - c.inv_bytes[d]);
     r->inv_leaves.push_back({si, &c, bs.get(), sb.get(), gb.get(), (int32_t)sel.size(), ngroups, seg->num_docs,
-                             sel_bytes + 2.0 * (double)((seg->num_docs + 7) / 8)});
+                             sel_bytes, 2.0 * (double)((seg->num_docs + 7) / 8)});
     if (!sel.empty() && c.inv.n < ((size_t)1 << 32)) {  // packed descriptors, built once per plan
       auto pb = std::make_unique<DevBuf>();
       rc = pb->alloc(sel.size() * 8);
@@ -2043,6 +2061,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   r->srv_order = Q.order_by;
   r->srv_min_trim = Q.min_trim;
   r->srv_trim_threshold = Q.trim_threshold;
+  r->srv_final = Q.server_final;
+  r->srv_sort_threshold = Q.sort_agg_threshold;
+  {  // QueryContext.isSameOrderAndGroupByColumns: the ORDER BY expressions, as a set, are the GROUP BY ones
+    std::vector<bool> seen(Q.group_by.size(), false);
+    bool only_keys = !Q.order_by.empty();
+    for (const auto& ob : Q.order_by) {
+      if (ob.kind != 0) only_keys = false;
+      else seen[ob.index] = true;
+    }
+    r->srv_safe = only_keys && std::all_of(seen.begin(), seen.end(), [](bool b) { return b; });
+  }
   double dense_keys = 1;
   for (size_t j = 0; j < Q.group_by.size(); ++j) {
     const std::string& g = Q.group_by[j];
@@ -2131,6 +2160,26 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
   r->limit_possible = limit_possible;
+  // Safe trim with LIMIT >= sortAggregateLimitThreshold and no serverReturnFinalResult: every segment keeps its
+  // top LIMIT groups by the ORDER BY (GroupByOperator.java:146-182, QueryContext.java:568-580) and the combine
+  // table keeps the top trimSize of their union, so groups past the global top LIMIT carry partial results. A
+  // segment that cannot hold more than LIMIT groups trims nothing; a segment-level trim is not restated here.
+  if (r->srv_safe && r->srv_limit >= 0 && r->srv_limit >= r->srv_sort_threshold && !r->srv_final && !filter_only &&
+      !Q.group_by.empty()) {
+    auto over = [&]() {
+      for (int si = 0; si < n; ++si)
+        if (seg_bound[si] > r->srv_limit) return true;
+      return false;
+    };
+    if (over() && !Q.preds.empty() && seg_matched.empty()) {
+      if (int rc = probe_matched()) return rc;
+      for (int si = 0; si < n; ++si) seg_bound[si] = std::min(seg_bound[si], seg_matched[si]);
+    }
+    if (over())
+      return fail(PINOT_AMD_EUNSUPPORTED, "server result limit: a segment-level safe trim (ORDER BY = GROUP BY, "
+                                          "LIMIT %lld >= sortAggregateLimitThreshold %lld) would drop groups",
+                  (long long)r->srv_limit, (long long)r->srv_sort_threshold);
+  }
   // admission prefixes (dense trimming): the docs of segment si that should hold numGroupsLimit distinct
   // keys, twice the coupon-collector expectation for K uniform keys (K ln(K / (K - L)) matching docs,
   // scaled by the segment's selectivity) plus 64 Ki docs; a segment that cannot reach the limit needs
@@ -2830,11 +2879,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           jl.mask = maxc <= 32 ? 1 : 2;
           jl.bits_regs = 0;
           // fixed-bit columns of <= 6 bits in 256-thread scan / select blocks: an LDS accept table per
-          // (clause, column), one lookup per 4 docs (<= 3 bits) or per 2 docs (4-6 bits)
+          // (clause, column) indexed by F = 4, 2 or 1 packed fields (4 / F lookups per lane of 4 docs). A
+          // table of <= 2^8 bytes spans <= 64 dwords, one per LDS bank, so a wave's 64 random lookups never
+          // conflict (lanes reading one dword broadcast); larger tables (the round-3 4-field tables of 3-bit
+          // columns: 4 KiB) cost ~6 conflict cycles per lookup (pmc_ssb11). PINOT_AMD_LUT_MAX_BITS raises the cap.
           const JitSlot& js = jp.slots[jl.slot];
+          static const int lut_max = (int)std::min<int64_t>(12, std::max<int64_t>(6, env_i64("PINOT_AMD_LUT_MAX_BITS", 8)));
           if (js.enc == ENC_FIXED_BIT && js.bits >= 1 && js.bits <= 6 && !jp.partitioned &&
               (jp.scan_nsub == 1 || jp.select) && !env_is("PINOT_AMD_LEAF_LUT", "0"))
-            jl.lut = js.bits <= 3 ? 4 * js.bits : 2 * js.bits;
+            jl.lut = 4 * js.bits <= lut_max ? 4 * js.bits : 2 * js.bits <= lut_max ? 2 * js.bits : js.bits;
         }
       }
       // larger dictId sets (<= 4096 words) are read from LDS, not from global memory per doc, by the
@@ -3278,7 +3331,11 @@ int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes) {
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
   double b = 0;
-  for (const auto& il : r->inv_leaves) b += il.alg_bytes;
+  // inverted leaves: the selected bitmaps' bytes; the dense bitset written and read back only when the
+  // expansion kernel runs (the fused inverted select of -fwselect plans keeps its words on-die)
+  bool all_fused = !r->launches.empty();
+  for (const auto& L : r->launches) all_fused &= L.fused;
+  for (const auto& il : r->inv_leaves) b += il.alg_bytes + (all_fused ? 0.0 : il.bitset_bytes);
   for (size_t li = 0; li < r->launches.size(); ++li) {
     const Launch& L = r->launches[li];
     if (L.select) {  // filter columns of every doc, the vector written and read, the gathered columns
@@ -3557,6 +3614,12 @@ static int server_trim(pinot_amd_result* r) {
   int64_t keep;
   if (r->srv_order.empty()) {
     keep = r->srv_limit;
+  } else if ((r->srv_safe && r->srv_limit < r->srv_sort_threshold) || r->srv_final) {
+    // safe trim with a small LIMIT: the sorted combine (SortedGroupByCombineOperator, CombinePlanNode.java:
+    // 150-154) merges the segments' top-LIMIT records keeping LIMIT (GroupByUtils.getSortedReduceMerger);
+    // every group of the global top LIMIT is in each of its segments' top LIMIT, so those are exact.
+    // serverReturnFinalResult without HAVING: the IndexedTable's result size is LIMIT (GroupByUtils.java:134)
+    keep = r->srv_limit;
   } else {
     keep = r->srv_min_trim > 0 ? std::max<int64_t>(r->srv_limit * 5, r->srv_min_trim) : INT64_MAX;
   }
@@ -3768,6 +3831,18 @@ static int key_pack(const pinot_amd_result* r, DevKeyPack* kp) {
 // accumulators exported per group: every array but the trimming plans' first-docId (always last)
 static int export_nacc(const pinot_amd_result* r) { return r->fd_acc >= 0 ? r->fd_acc : r->q.nacc; }
 
+// the stream a cross-rank call runs on: the caller's (ordered after the result's own stream through an
+// event, whatever the caller did), or the result's; r->stream itself is never replaced
+static int call_stream(pinot_amd_result* r, void* stream, hipStream_t* out) {
+  *out = r->stream;
+  if (!stream || (hipStream_t)stream == r->stream) return 0;
+  if (!r->ev_x) HIP_OK(hipEventCreateWithFlags(&r->ev_x, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(r->ev_x, r->stream));
+  HIP_OK(hipStreamWaitEvent((hipStream_t)stream, r->ev_x, 0));
+  *out = (hipStream_t)stream;
+  return 0;
+}
+
 int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64_t* d_acc, int64_t cap,
                                    int32_t* h_key_words, int32_t* h_num_acc, int64_t* h_num_groups, void* stream) {
   if (!r || !h_key_words || !h_num_acc || !h_num_groups || cap < 0)
@@ -3775,25 +3850,28 @@ int pinot_amd_result_export_groups(pinot_amd_result* r, uint64_t* d_keys, uint64
   return no_throw("export_groups", [&]() -> int {
     if (r->num_group_by == 0 || r->q.nacc == 0)
       return fail(PINOT_AMD_EUNSUPPORTED, "export_groups: not a GROUP BY result with aggregations");
-    if (r->merged) return fail(PINOT_AMD_EINVAL, "export_groups: result already merged");
-    if (stream) r->stream = (hipStream_t)stream;
+    hipStream_t st;
+    if (int rc = call_stream(r, stream, &st)) return rc;
     DevKeyPack kp;
     if (int rc = key_pack(r, &kp)) return rc;
-    if (r->kind == PLAN_HASH && kp.nw != r->nw) return fail(PINOT_AMD_EINVAL, "export_groups: key packing mismatch");
+    // a merged result exports its merged table (keys already packed this way: a key-partitioned
+    // cross-rank merge exports each rank's merged share again)
+    if (!r->merged && r->kind == PLAN_HASH && kp.nw != r->nw)
+      return fail(PINOT_AMD_EINVAL, "export_groups: key packing mismatch");
+    if (r->merged && kp.nw != r->mnw) return fail(PINOT_AMD_EINVAL, "export_groups: merged key packing mismatch");
     if (int rc = check_overflow(r)) return rc;
     const GroupTable T = group_table(r);
     const DevBuf& idx = r->c_idx;
     int64_t ng = 0;
-    if (int rc = compact_slots(r, T, r->stream, &ng)) return rc;
+    if (int rc = compact_slots(r, T, st, &ng)) return rc;
     *h_key_words = kp.nw;
     *h_num_acc = export_nacc(r);
     *h_num_groups = ng;
     if (!d_keys || !d_acc) return 0;  // sizing call
     if (ng > cap) return fail(PINOT_AMD_EOVERFLOW, "export_groups: %lld groups exceed capacity %lld", (long long)ng,
                               (long long)cap);
-    HIP_OK(launch_export_groups((const int32_t*)idx.p, ng, T.keys, T.slots, T.acc, export_nacc(r), kp, d_keys, d_acc,
-                                r->stream));
-    HIP_OK(hipStreamSynchronize(r->stream));
+    HIP_OK(launch_export_groups((const int32_t*)idx.p, ng, T.keys, T.slots, T.acc, export_nacc(r), kp, d_keys, d_acc, st));
+    HIP_OK(hipStreamSynchronize(st));
     return 0;
   });
 }
@@ -3804,24 +3882,23 @@ int pinot_amd_result_merge_groups(pinot_amd_result* r, const uint64_t* d_keys, c
   return no_throw("merge_groups", [&]() -> int {
     if (r->num_group_by == 0 || r->q.nacc == 0)
       return fail(PINOT_AMD_EUNSUPPORTED, "merge_groups: not a GROUP BY result with aggregations");
-    if (stream) r->stream = (hipStream_t)stream;
-    hipStream_t st = r->stream;
+    hipStream_t st;
+    if (int rc = call_stream(r, stream, &st)) return rc;
     DevKeyPack kp;
     if (int rc = key_pack(r, &kp)) return rc;
     r->merged = false;
-    r->mcap = next_pow2(std::max<int64_t>(64, 2 * n));
-    if (r->mcap > ((int64_t)1 << 31)) return fail(PINOT_AMD_EUNSUPPORTED, "merge_groups: %lld rows", (long long)n);
+    const int64_t mcap = next_pow2(std::max<int64_t>(64, 2 * n));
+    if (mcap > ((int64_t)1 << 31)) return fail(PINOT_AMD_EUNSUPPORTED, "merge_groups: %lld rows", (long long)n);
+    // the merged table's buffers grow and are reused across merges (one per step in a multi-GPU loop)
+    if (int rc = r->mkeys.ensure((size_t)mcap * kp.nw * 8)) return rc;
+    if (int rc = r->macc.ensure((size_t)mcap * r->q.nacc * 8)) return rc;
+    if (int rc = r->movf.ensure(8)) return rc;
+    r->mcap = mcap;
     r->mnw = kp.nw;
-    r->mkeys.reset();
-    r->macc.reset();
-    r->movf.reset();
-    if (int rc = r->mkeys.alloc((size_t)r->mcap * kp.nw * 8)) return rc;
-    if (int rc = r->macc.alloc((size_t)r->mcap * r->q.nacc * 8)) return rc;
-    if (int rc = r->movf.alloc(8)) return rc;
-    HIP_OK(hipMemsetAsync(r->mkeys.p, 0xFF, r->mkeys.n, st));
+    HIP_OK(hipMemsetAsync(r->mkeys.p, 0xFF, (size_t)mcap * kp.nw * 8, st));
     HIP_OK(hipMemsetAsync(r->movf.p, 0, 8, st));
-    HIP_OK(launch_init_acc((uint64_t*)r->macc.p, r->q, r->mcap, st));
-    HIP_OK(launch_merge_rows(d_keys, d_acc, n, kp.nw, export_nacc(r), (unsigned long long*)r->mkeys.p, r->mcap,
+    HIP_OK(launch_init_acc((uint64_t*)r->macc.p, r->q, mcap, st));
+    HIP_OK(launch_merge_rows(d_keys, d_acc, n, kp.nw, export_nacc(r), (unsigned long long*)r->mkeys.p, mcap,
                              (uint64_t*)r->macc.p, r->q, (unsigned long long*)r->movf.p, st));
     unsigned long long ovf = 0;
     HIP_OK(hipMemcpyAsync(&ovf, r->movf.p, 8, hipMemcpyDeviceToHost, st));

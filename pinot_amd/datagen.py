@@ -66,6 +66,15 @@ BENCH_QUERY = ("SELECT daysSinceEpoch, COUNT(*), SUM(clicks), SUM(impressions), 
                f"WHERE daysSinceEpoch BETWEEN {DAYS_BASE + 100} AND {DAYS_BASE + 300} AND clicks > 100 "
                "GROUP BY daysSinceEpoch")
 
+# BASELINE.json configs[0]: the reference README's AdAnalytics example query (README.md:95-100: an 8-day
+# daysSinceEpoch range AND accountId IN (...), SUM(clicks), SUM(impressions) GROUP BY daysSinceEpoch),
+# with the bench table's `country` dimension in the role of accountId (Pinot's TOP n is LIMIT n)
+README_QUERY = ("SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM AdAnalyticsTable "
+                f"WHERE ((daysSinceEpoch >= {DAYS_BASE + 249} AND daysSinceEpoch <= {DAYS_BASE + 256})) "
+                "AND country IN (7, 42, 123) GROUP BY daysSinceEpoch LIMIT 100")
+# its column bytes per row: 9-bit daysSinceEpoch + 8-bit country + 4 B clicks + 8 B impressions
+README_BYTES_PER_ROW = (S.num_bits_per_value(NUM_DAYS - 1) + S.num_bits_per_value(NUM_COUNTRIES - 1)) / 8.0 + 4 + 8
+
 # Algorithmic HBM bytes per row of BENCH_QUERY: every referenced column is read once
 # (9-bit daysSinceEpoch + 4 B clicks + 8 B impressions + 8 B cost); group accumulators stay in LDS.
 BENCH_BYTES_PER_ROW = S.num_bits_per_value(NUM_DAYS - 1) / 8.0 + 4 + 8 + 8

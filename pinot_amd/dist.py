@@ -7,8 +7,10 @@ in-kernel), and the tables of all GPUs are merged in place with RCCL all-reduces
 SUM/COUNT as int64 or fp64 sums, MIN/MAX as min/max of an order-preserving int64 encoding of the
 double value. Small tables go through one all-gather reduced locally; no other data-path collective.
 Results without a shared dense table (hash-table plans, numGroupsLimit trimming, DISTINCTCOUNT) merge
-by value on the device: one all-gather of every rank's compacted (key words, accumulator words) rows,
-folded into one device hash table by the library.
+by value on the device, partitioned by key: every rank's compacted (key words, accumulator words) rows go
+to the rank that owns their key hash (one all-to-all), each rank folds its 1/N share into a device hash
+table (the library's merge), and the merged shares -- disjoint -- are all-gathered so every rank ends up
+with the final groups (or only rank `root` receives them).
 
 Every rank plans the query over the same group key space: ``global_key_space`` all-gathers each
 rank's group-by column values and the union is installed on every rank
@@ -149,16 +151,18 @@ class _DeviceWords:
                                          "strides": None}
 
 
-def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes: int = 1 << 20):
-    """Merge a query result across ranks; afterwards every rank's result holds the merged groups.
+def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes: int = 1 << 20, root=None):
+    """Merge a query result across ranks; afterwards every rank's result holds the merged groups (with
+    `root` set, only that rank's; the others hold their key-partitioned share).
 
-    The ranks first agree on HOW (one all-reduce of a flag): when every rank's result keeps its groups in
+    The ranks first agree on HOW (one all-reduce of two flags: "some rank needs a merge by value" and
+    numGroupsLimitReached, which the broker ORs over servers): when every rank's result keeps its groups in
     a dense accumulator table (identical key space via global_key_space) the tables are merged in place
     (merge_tables on a zero-copy torch view of the library's HBM table); when any rank ran a hash-table
-    plan (large key spaces, numGroupsLimit trimming) or the query has DISTINCTCOUNT, every rank merges BY
-    VALUE on the device: export_groups -> one all-gather of the (key words, accumulator words) rows ->
-    merge_groups folds all ranks' rows into one device hash table (GroupByDataTableReducer's merge). A
-    rank never decides alone, so ranks whose plans differ still run the same collectives.
+    plan (large key spaces, numGroupsLimit trimming) or the query has DISTINCTCOUNT, grouped parts merge BY
+    VALUE on the device, partitioned by key (merge_by_value); aggregation-only parts (DISTINCTCOUNT's base
+    query without GROUP BY) still merge in place. A rank never decides alone, so ranks whose plans differ
+    still run the same collectives.
 
     `stream`: the stream the result was executed on; torch's current stream waits for it first.
     `scratch` is unused (kept for callers)."""
@@ -176,17 +180,17 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
         return scratch
     # DISTINCTCOUNT folds (group key, value) groups whose value column is not in the dense key space
     local_by_value = hasattr(result, "results") or any(not p.has_dense_table() for p in parts)
+    reached = any(_limit_reached(p) for p in parts)
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    flag = torch.tensor([1 if local_by_value else 0], dtype=torch.int64, device=dev)
+    flag = torch.tensor([1 if local_by_value else 0, 1 if reached else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    if int(flag.item()):
-        for p in parts:
-            keys, acc = p.export_groups(stream=cur)
-            rows = gather_rows(torch.cat([keys, acc], dim=1), group)
-            kw = keys.shape[1]
-            p.merge_groups(rows[:, :kw].contiguous(), rows[:, kw:].contiguous(), stream=cur)
-        return scratch
+    by_value, reached_any = (bool(x) for x in flag.tolist())
     for p in parts:
+        if hasattr(p, "set_merged_limit_reached"):
+            p.set_merged_limit_reached(reached_any)
+        if by_value and _grouped(p):
+            merge_by_value(p, group, cur, root)
+            continue
         ops, nk, ptrs = p.accumulators()
         if not ops:
             continue
@@ -196,7 +200,67 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
     return scratch
 
 
-def gather_rows(rows, group=None):
+def _grouped(p) -> bool:
+    qc = getattr(p, "qc", None)
+    return True if qc is None else bool(qc.group_by)
+
+
+def _limit_reached(p) -> bool:
+    f = getattr(p, "num_groups_limit_reached", None)
+    return bool(f()) if f is not None else False
+
+
+def key_owner(keys, world: int):
+    """Rank owning each row's group: a multiplicative hash of its key words (int64 arithmetic wraps),
+    high bits folded, modulo the world size. Identical on every rank for identical key words."""
+    h = keys[:, 0] * -7046029254386353131
+    for w in range(1, keys.shape[1]):
+        h = (h ^ keys[:, w]) * -7046029254386353131
+    return ((h >> 33) & 0x3FFFFFFF) % world
+
+
+def exchange_rows(rows, dest, group=None):
+    """All-to-all of [n, w] int64 rows: row i goes to rank dest[i]. Returns this rank's received rows (in
+    source-rank order). One all-to-all of the counts, one of the rows."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    order = torch.argsort(dest, stable=True)
+    send = rows[order].contiguous()
+    send_counts = torch.bincount(dest, minlength=world).to(torch.int64)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    recv = rows.new_empty((sum(rc), rows.shape[1]))
+    dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    return recv
+
+
+def merge_by_value(p, group=None, stream=None, root=None):
+    """GroupByDataTableReducer's merge (GroupByDataTableReducer.java:258) across ranks, partitioned by key:
+    export_groups -> all-to-all by key owner -> merge_groups of this rank's share (each group's partials
+    meet on one rank, so 1/N of the rows per rank) -> the merged shares, disjoint, all-gathered (or
+    gathered on `root`) -> merge_groups again, which only inserts them."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    keys, acc = p.export_groups(stream=stream)
+    kw = keys.shape[1]
+    rows = torch.cat([keys, acc], dim=1)
+    mine = exchange_rows(rows, key_owner(keys, world), group)
+    p.merge_groups(mine[:, :kw].contiguous(), mine[:, kw:].contiguous(), stream=stream)
+    mk, ma = p.export_groups(stream=stream)
+    share = torch.cat([mk, ma], dim=1)
+    if root is None:
+        allr = gather_rows(share, group)
+    else:
+        allr = gather_rows_to(share, root, group)
+        if dist.get_rank(group) != root:
+            return
+    p.merge_groups(allr[:, :kw].contiguous(), allr[:, kw:].contiguous(), stream=stream)
+
+
+def gather_rows(rows, group=None, return_counts: bool = False):
     """All-gather every rank's [n_r, w] int64 rows (n_r may differ) into the concatenation in rank order:
     one all-gather of the row counts, one of the rows padded to the largest count."""
     import torch
@@ -209,11 +273,36 @@ def gather_rows(rows, group=None):
     m = max(counts)
     w = rows.shape[1]
     if m == 0:
-        return rows.new_empty((0, w))
+        out = rows.new_empty((0, w))
+        return (out, counts) if return_counts else out
     buf = rows.new_zeros((m, w))
     buf[:rows.shape[0]] = rows
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
+    out = torch.cat([p[:c] for p, c in zip(parts, counts)]).contiguous()
+    return (out, counts) if return_counts else out
+
+
+def gather_rows_to(rows, root: int, group=None):
+    """gather_rows onto one rank (the broker's view): the rows of every rank in rank order on `root`, an
+    empty tensor elsewhere. Counts travel by all-gather (tiny), rows by one gather."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    counts = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m, w = max(counts), rows.shape[1]
+    if m == 0:
+        return rows.new_empty((0, w))
+    buf = rows.new_zeros((m, w))
+    buf[:rows.shape[0]] = rows
+    me = dist.get_rank(group)
+    parts = [torch.empty_like(buf) for _ in range(world)] if me == root else None
+    dist.gather(buf, parts, dst=root, group=group)
+    if me != root:
+        return rows.new_empty((0, w))
     return torch.cat([p[:c] for p, c in zip(parts, counts)]).contiguous()
 
 
@@ -267,14 +356,44 @@ def key_columns(qc) -> list:
 
 
 def _value_kind(vals) -> str:
-    """'i' (all Python ints), 'f' (all floats), '-' (none), 'o' (strings / mixed)."""
+    """'i' (all Python ints), 'f' (all floats), 's' (all strings), '-' (none), 'o' (mixed)."""
     if not vals:
         return "-"
     if all(isinstance(v, int) and not isinstance(v, bool) for v in vals):
         return "i"
     if all(isinstance(v, float) for v in vals):
         return "f"
+    if all(isinstance(v, str) for v in vals):
+        return "s"
     return "o"
+
+
+def _gather_strings(vals, group=None) -> list:
+    """Every rank's strings, concatenated in rank order, as tensors over the process group (no pickling):
+    the UTF-8 byte lengths as [n, 1] int64 rows and the concatenated bytes packed 8 per int64 row, each
+    through gather_rows (which also returns each rank's row counts, to cut the byte blob per rank)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    enc = [v.encode("utf-8") for v in vals]
+    lens = np.asarray([len(b) for b in enc], dtype=np.int64)
+    blob = b"".join(enc)
+    blob += b"\0" * ((-len(blob)) % 8)
+    words = np.frombuffer(blob, dtype=np.int64) if blob else np.zeros(0, dtype=np.int64)
+    all_lens, nstr = gather_rows(torch.from_numpy(lens.reshape(-1, 1).copy()).to(dev), group, return_counts=True)
+    all_words, _ = gather_rows(torch.from_numpy(words.reshape(-1, 1).copy()).to(dev), group, return_counts=True)
+    all_lens = all_lens.cpu().numpy().reshape(-1)
+    data = all_words.cpu().numpy().reshape(-1).tobytes()
+    out, li, pos = [], 0, 0
+    for c in nstr:  # rank by rank: its strings, then its blob padded to 8 bytes
+        start = pos
+        for n in all_lens[li:li + c].tolist():
+            out.append(data[pos:pos + n].decode("utf-8"))
+            pos += n
+        li += c
+        pos = start + ((pos - start + 7) // 8) * 8
+    return out
 
 
 def _gather_numeric(vals, kind: str, group=None) -> list:
@@ -296,8 +415,9 @@ def global_key_space(segments, group_by: Sequence[str], group=None, executor=Non
     ServerQueryExecutor.execute(..., key_space=...) so that every rank's dense group table indexes the
     same groups and merge_result can all-reduce them in place. Numeric columns travel as int64 tensors
     (one all-gather of counts, one of the padded values: million-value raw key columns never go through
-    pickling); string columns, or ranks disagreeing on a column's value kind, through all_gather_object.
-    The union keeps the first occurrence in rank order."""
+    pickling), STRING columns as UTF-8 lengths + bytes packed in int64 tensors (_gather_strings); only ranks
+    disagreeing on a column's value kind fall back to all_gather_object. The union keeps the first
+    occurrence in rank order."""
     import torch.distributed as dist
     from .query import distinct_value
     mine = {g: local_key_values(segments, g, executor) for g in group_by}
@@ -311,6 +431,8 @@ def global_key_space(segments, group_by: Sequence[str], group=None, executor=Non
             ks = {k[g] for k in kinds} - {"-"}
             if len(ks) == 1 and ks <= {"i", "f"}:
                 gathered[g] = _gather_numeric(mine[g], ks.pop(), group)
+            elif ks == {"s"}:
+                gathered[g] = _gather_strings(mine[g], group)
             elif not ks:
                 gathered[g] = []
             else:

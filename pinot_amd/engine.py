@@ -25,7 +25,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import ColumnSpec, PredicateSpec, check, lib
-from .query import JavaDouble, QueryContext, fold_distinct_count, parse_sql, reduce_rows, split_distinct_count
+from .query import (JavaDouble, QueryContext, fold_distinct_count, parse_sql, reduce_rows, server_table,
+                    split_distinct_count)
 from .segment import ColumnBuffers, SegmentBuffers, DOUBLE, FLOAT, INT, LONG, STRING
 
 TYPE_CODE = {INT: 0, LONG: 1, FLOAT: 2, DOUBLE: 3, STRING: 4}
@@ -160,8 +161,9 @@ class DistinctCountResult:
     """Result of a query with DISTINCTCOUNT aggregations (query.split_distinct_count): the base
     result plus one grouped result per DISTINCTCOUNT, folded into per-group value sets."""
 
-    def __init__(self, qc, base, subs):
+    def __init__(self, qc, base, subs, server_trim: bool = False):
         self.qc, self._base, self._subs = qc, base, subs
+        self._server_trim = server_trim  # the server's combine table over the folded groups
 
     def num_docs_matched(self) -> int:
         return self._base.num_docs_matched()
@@ -176,7 +178,8 @@ class DistinctCountResult:
         return [self._base] + [r for _, r in self._subs]
 
     def groups(self):
-        return fold_distinct_count(self.qc, self._base.groups(), [(i, r.groups()) for i, r in self._subs])
+        g = fold_distinct_count(self.qc, self._base.groups(), [(i, r.groups()) for i, r in self._subs])
+        return server_table(self.qc, g) if self._server_trim else g
 
     def rows(self):
         return reduce_rows(self.qc, self.groups())
@@ -214,9 +217,16 @@ class QueryResult:
         self.qc = qc
         self._agg_slots = agg_slots      # per qc aggregation: ('direct', native_idx) | ('avg', sum_idx)
         self._key_types = key_types
+        self._merged_reached = None      # numGroupsLimitReached OR-ed over ranks by dist.merge_result
 
     def execute_again(self, stream=None) -> None:
+        self._merged_reached = None
         check(lib().pinot_amd_execute_again(self._h, _stream_handle(stream)), "execute_again")
+
+    def set_merged_limit_reached(self, reached: bool) -> None:
+        """The broker ORs numGroupsLimitReached over servers (BrokerReduceService): after a cross-rank
+        merge every rank reports the OR of all ranks' flags, until the next execution."""
+        self._merged_reached = bool(reached)
 
     def num_docs_matched(self) -> int:
         out = C.c_int64()
@@ -224,7 +234,10 @@ class QueryResult:
         return out.value
 
     def num_groups_limit_reached(self) -> bool:
-        """GroupByResultsBlock.isNumGroupsLimitReached: more groups than the numGroupsLimit option."""
+        """GroupByResultsBlock.isNumGroupsLimitReached: more groups than the numGroupsLimit option (after
+        dist.merge_result: the OR over every rank's)."""
+        if self._merged_reached is not None:
+            return self._merged_reached
         out = C.c_int32()
         check(lib().pinot_amd_result_num_groups_limit_reached(self._h, C.byref(out)), "num_groups_limit_reached")
         return bool(out.value)
@@ -318,11 +331,12 @@ class QueryResult:
                                                         C.byref(got2)), "fetch_intermediate")
         return got, keys, vals, vals_i, pairs
 
-    def groups(self) -> Dict[tuple, list]:
+    def groups(self, arrays=None) -> Dict[tuple, list]:
         """key tuple (group-by values; () for aggregation-only) -> intermediate result per aggregation.
-        Converted column-wise (numpy -> Python lists, zipped), not group by group."""
+        Converted column-wise (numpy -> Python lists, zipped), not group by group. `arrays`: the output of
+        an earlier fetch_arrays() of this execution (not fetched again)."""
         L = lib()
-        got, keys, vals, vals_i, pairs = self.fetch_arrays()
+        got, keys, vals, vals_i, pairs = self.fetch_arrays() if arrays is None else arrays
         n = got.value
         nk = len(self.qc.group_by)
         nnat = max(len(self._native_aggs), 1)
@@ -446,9 +460,17 @@ class ServerQueryExecutor:
         every rank's dense group table indexes the same groups."""
         qc = parse_sql(query) if isinstance(query, str) else query
         if any(a.func == "DISTINCTCOUNT" for a in qc.aggregations):
+            # the device queries run untrimmed (a result limit on a (group, value) sub-query would cut value
+            # sets); the server's combine table applies to the folded groups (DistinctCountResult.groups)
+            trim = self.server_trim and bool(qc.group_by)
+            if trim and qc.safe_trim() and qc.limit >= qc.sort_aggregate_limit_threshold \
+                    and not qc.server_return_final_result:
+                raise _lib.PinotAmdError("DISTINCTCOUNT with a segment-level safe trim (ORDER BY = GROUP BY, LIMIT >= "
+                                         "sortAggregateLimitThreshold) is not supported with server_trim")
             base, subs = split_distinct_count(qc)
-            return DistinctCountResult(qc, self._execute(base, segments, stream, key_space),
-                                       [(i, self._execute(sq, segments, stream, key_space)) for i, sq in subs])
+            return DistinctCountResult(qc, self._execute(base, segments, stream, key_space, server_trim=False),
+                                       [(i, self._execute(sq, segments, stream, key_space, server_trim=False))
+                                        for i, sq in subs], server_trim=trim)
         return self._execute(qc, segments, stream, key_space)
 
     @staticmethod
@@ -464,9 +486,11 @@ class ServerQueryExecutor:
         check(lib().pinot_amd_query_set_group_key_values(qh, column.encode(), TYPE_CODE[stored_type], n, vi, vd, vs),
               f"set_group_key_values({column})")
 
-    def _execute(self, qc, segments: Sequence[ImmutableSegment], stream=None, key_space=None) -> QueryResult:
+    def _execute(self, qc, segments: Sequence[ImmutableSegment], stream=None, key_space=None,
+                 server_trim=None) -> QueryResult:
         if not segments:
             raise ValueError("no segments")
+        server_trim = self.server_trim if server_trim is None else server_trim
         L = lib()
         first = segments[0]
         qh = C.c_void_p()
@@ -485,9 +509,11 @@ class ServerQueryExecutor:
                 if key_space is not None and g in key_space:
                     self._set_key_space(qh, g, first.columns[g].stored_type, key_space[g])
             check(L.pinot_amd_query_set_num_groups_limit(qh, qc.num_groups_limit), "set_num_groups_limit")
-            if self.server_trim and qc.group_by:
+            if server_trim and qc.group_by:
                 check(L.pinot_amd_query_set_result_limit(qh, qc.limit, qc.min_server_group_trim_size,
                                                          qc.group_trim_threshold), "set_result_limit")
+                check(L.pinot_amd_query_set_server_options(qh, 1 if qc.server_return_final_result else 0,
+                                                           qc.sort_aggregate_limit_threshold), "set_server_options")
             native = []
             agg_slots = []
 
@@ -515,7 +541,7 @@ class ServerQueryExecutor:
                     agg_slots.append(("direct", add(a.func, a.column, a.expr)))
             if not qc.aggregations and qc.group_by:
                 add("COUNT", "*")  # DISTINCT-style group-by still needs the group presence count
-            if self.server_trim and qc.group_by:
+            if server_trim and qc.group_by:
                 for kind, idx, asc in qc.order_by_targets():
                     if kind == 1:  # the library aggregation whose final value orders (AVG: sum / count)
                         a = qc.aggregations[idx]

@@ -141,6 +141,17 @@ class QueryContext:
     # the server combine table's trim options (QueryOptionsUtils: minServerGroupTrimSize, groupTrimThreshold)
     min_server_group_trim_size: int = 5000
     group_trim_threshold: int = 1_000_000
+    # serverReturnFinalResult, sortAggregateLimitThreshold (CommonConstants: default 10000)
+    server_return_final_result: bool = False
+    sort_aggregate_limit_threshold: int = 10_000
+
+    def safe_trim(self) -> bool:
+        """QueryContext._isUnsafeTrim is false: the ORDER BY expressions, as a set, are the GROUP BY ones (no
+        HAVING in this subset) -- QueryContext.java:746-747, isSameOrderAndGroupByColumns."""
+        if not self.group_by or not self.order_by:
+            return False
+        t = self.order_by_targets()
+        return all(k == 0 for k, _, _ in t) and {i for _, i, _ in t} == set(range(len(self.group_by)))
 
     def order_by_targets(self) -> List[Tuple[int, int, bool]]:
         """ORDER BY as (kind, index, ascending): kind 0 = group-by column index, 1 = aggregation index
@@ -422,8 +433,8 @@ def _query_options(sql: str):
 
 def parse_sql(sql: str) -> QueryContext:
     """Compile a Pinot SQL query of the supported subset into a QueryContext. The numGroupsLimit,
-    minServerGroupTrimSize and groupTrimThreshold query options (QueryOptionsUtils) are honoured; other
-    options are ignored."""
+    minServerGroupTrimSize, groupTrimThreshold, serverReturnFinalResult and sortAggregateLimitThreshold query
+    options (QueryOptionsUtils) are honoured; other options are ignored."""
     sql, opts = _query_options(sql)
     qc = _Parser(sql).query()
     for k, v in opts.items():
@@ -433,6 +444,10 @@ def parse_sql(sql: str) -> QueryContext:
             qc.min_server_group_trim_size = int(v)
         elif k.lower() == "grouptrimthreshold":
             qc.group_trim_threshold = int(v)
+        elif k.lower() == "serverreturnfinalresult":
+            qc.server_return_final_result = v.strip().lower() == "true"
+        elif k.lower() == "sortaggregatelimitthreshold":
+            qc.sort_aggregate_limit_threshold = int(v)
     return qc
 
 
@@ -547,6 +562,63 @@ def fold_distinct_count(qc: QueryContext, base_groups: dict, sub_groups: Sequenc
             full[i] = frozenset(sets[i].get(ck, ()))
         out[key] = full
     return out
+
+
+def _dict_order(v):
+    """A group-by value's position key in its (merged) dictionary's order: numbers ascending with
+    Double.compare semantics for floats (-0.0 before 0.0, NaN last), strings by UTF-16 code units."""
+    if isinstance(v, str):
+        return (0, v.encode("utf-16-be"))
+    if isinstance(v, float):
+        return (1, (1, 0.0, 0) if math.isnan(v) else (0, v, int(math.copysign(1.0, v) > 0)))
+    return (1, (0, v, 0))
+
+
+def _double_order(x):
+    x = float(x)
+    return (1, 0.0, 0) if math.isnan(x) else (0, x, int(math.copysign(1.0, x) > 0))
+
+
+class _Reverse:
+    __slots__ = ("k",)
+
+    def __init__(self, k):
+        self.k = k
+
+    def __lt__(self, o):
+        return o.k < self.k
+
+    def __eq__(self, o):
+        return self.k == o.k
+
+
+def server_table(qc: QueryContext, groups: dict) -> dict:
+    """The server's combine table over combined groups, as the library applies it at compaction
+    (pinot_amd_query_set_result_limit / set_server_options; GroupByUtils.java:104-149, IndexedTable.finish):
+    no ORDER BY -> the first LIMIT groups in ascending key order (last group-by column compared first);
+    ORDER BY -> sorted by it (ties in ascending key order) and cut to LIMIT under a safe trim below
+    sortAggregateLimitThreshold or with serverReturnFinalResult, else to trimSize = max(5 * LIMIT,
+    minServerGroupTrimSize) (no cut when that option is <= 0)."""
+    keys = sorted(groups, key=lambda k: tuple(_dict_order(v) for v in reversed(k)))
+    if not qc.order_by:
+        return {k: groups[k] for k in keys[:qc.limit]}
+    rank = {k: i for i, k in enumerate(keys)}
+    targets = qc.order_by_targets()
+
+    def sort_key(k):
+        out = []
+        for kind, idx, asc in targets:
+            o = _dict_order(k[idx]) if kind == 0 else _double_order(final_value(qc.aggregations[idx].func, groups[k][idx]))
+            out.append(o if asc else _Reverse(o))
+        return tuple(out) + (rank[k],)
+    ordered = sorted(keys, key=sort_key)
+    if (qc.safe_trim() and qc.limit < qc.sort_aggregate_limit_threshold) or qc.server_return_final_result:
+        keep = qc.limit
+    elif qc.min_server_group_trim_size > 0:
+        keep = max(5 * qc.limit, qc.min_server_group_trim_size)
+    else:
+        keep = len(ordered)
+    return {k: groups[k] for k in ordered[:keep]}
 
 
 def reduce_rows(qc: QueryContext, groups: dict) -> List[tuple]:

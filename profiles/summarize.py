@@ -1,6 +1,7 @@
-"""Summarise profiles/profile_r03.sh outputs (gpurun_out/prof3/<workload>/) into profiles/r03/.
+"""Summarise profiles/profile.sh outputs (gpurun_out/prof_<round>/<workload>/) into profiles/<round>/.
 
-    python3 profiles/summarize_r03.py gpurun_out/prof3 profiles/r03
+    COMMIT=<rev> python3 profiles/summarize.py gpurun_out/prof_r04 <dst>   # on the GPU box
+    python3 profiles/summarize.py --index profiles/r04                    # rebuild pmc_index.json from pmc_*.json
 
 Per workload: kernel_stats_<w>.csv (rocprofv3 --stats copy) and pmc_<w>.json with, per kernel, the mean
 trace duration and the mean of every counter per dispatch; per execution of the query plan (all its
@@ -9,6 +10,8 @@ half the bytes of wide coalesced streaming reads on gfx950), write bytes = WRITE
 the plan's algorithmic bytes (the bench line's bytes_per_row x rows), and the plan's device time."""
 import csv
 import collections
+import glob
+import hashlib
 import json
 import os
 import shutil
@@ -48,7 +51,7 @@ def main(src, dst):
             durs[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
         plan = {k: v for k, v in durs.items() if len(v) >= execs_trace - 1 and
                 any(s in k for s in ("pinot", "roaring", "partition", "exclusive", "init_acc", "trim", "hash", "admit",
-                                     "allot", "merge", "pack_sel", "gather", "presence", "bitset"))}
+                                     "allot", "merge", "pack_sel", "gather", "presence", "bitset", "lhash"))}
         # A kernel with more dispatches than executions also ran the planner's filter-only match-count
         # probe (selection-vector cost model, numGroupsLimit bound): once in the cold execution since the
         # round-3 probe cache (dispatch 0), twice before it (dispatches 0 and 2). Plan-time work, dropped.
@@ -88,14 +91,33 @@ def main(src, dst):
             "achieved_GBps_from_trace": alg / (plan_ms / 1e3) / 1e9 if plan_ms else None,
             "bench_kernel_ms_hip_events": tb["roofline"]["kernel_ms"], "bench_frac": tb["roofline"]["frac"],
             "query": tb["config"]["query"],
+            # the bench line's full query hash and device plan: bench.py uses this record's traffic only for
+            # the same query on the same plan
+            "query_sha1": tb["config"].get("query_sha1") or hashlib.sha1(tb["config"]["query"].encode()).hexdigest(),
+            "scan_kernel": tb["config"]["scan_kernel"],
+            "commit": os.environ.get("COMMIT", "unknown"),
         }
         with open(os.path.join(dst, f"pmc_{w}.json"), "w") as f:
             json.dump(out, f, indent=1)
         index[w] = out["per_execution"]
+    build_index(dst)
+
+
+def build_index(dst):
+    """pmc_index.json of a profiles/<round>/ directory: workload -> per_execution of its pmc_<w>.json."""
+    index = {}
+    for p in sorted(glob.glob(os.path.join(dst, "pmc_*.json"))):
+        if os.path.basename(p) == "pmc_index.json":
+            continue
+        d = json.load(open(p))
+        index[d["workload"]] = d["per_execution"]
     with open(os.path.join(dst, "pmc_index.json"), "w") as f:
         json.dump(index, f, indent=1)
     print(json.dumps(index, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if sys.argv[1] == "--index":
+        build_index(sys.argv[2])
+    else:
+        main(sys.argv[1], sys.argv[2])

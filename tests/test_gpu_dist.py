@@ -41,6 +41,10 @@ def _segments():
 TRIM_QUERY = ("SET numGroupsLimit = 40; SELECT d1, COUNT(*), SUM(r_long), MIN(r_double), MAX(r_int) FROM t "
               "WHERE d0 < 4000 GROUP BY d1")
 DC_QUERY = "SELECT d1, DISTINCTCOUNT(r_int), COUNT(*), SUM(r_long) FROM t WHERE d0 < 3000 GROUP BY d1"
+# DISTINCTCOUNT without GROUP BY: its base query is aggregation-only (merged in place), the value-set query
+# merges by value (round-3 advisor: export_groups refused the base part)
+DC_AGG_QUERY = "SELECT DISTINCTCOUNT(d1), COUNT(*), SUM(r_long) FROM t WHERE d0 < 3000"
+QUERIES = {"trim": TRIM_QUERY, "distinct": DC_QUERY, "distinct_agg": DC_AGG_QUERY}
 
 
 def _worker(rank, world, port, q, plan):
@@ -59,7 +63,7 @@ def _worker(rank, world, port, q, plan):
     dist.all_gather_object(fps, pdist.key_space_fingerprint(bufs, ["d1"]))
     assert len(set(fps)) == world, "shards were meant to hold different dictionaries"
     segs = [engine.ImmutableSegment(b) for b in bufs]
-    query = {"trim": TRIM_QUERY, "distinct": DC_QUERY}.get(plan, QUERY)
+    query = QUERIES.get(plan, QUERY)
     ks = pdist.global_key_space(segs, pdist.key_columns(parse_sql(query)))
     res = engine.ServerQueryExecutor().execute(query, segs, stream=torch.cuda.current_stream(), key_space=ks)
     if plan == "dense":
@@ -79,7 +83,7 @@ def _worker(rank, world, port, q, plan):
 
 
 @pytest.mark.parametrize("plan,gather_max", [("dense", 0), ("dense", 1 << 20), ("hash", 0), ("mixed", 0), ("trim", 0),
-                                             ("distinct", 0)])
+                                             ("distinct", 0), ("distinct_agg", 0)])
 def test_two_rank_merge_equals_single_process(plan, gather_max, monkeypatch):
     """Every rank ends with the single-process result: dense plans through the in-place table merge;
     hash plans, a hash rank next to a dense rank (the ranks agree on the by-value merge), numGroupsLimit
@@ -100,16 +104,18 @@ def test_two_rank_merge_equals_single_process(plan, gather_max, monkeypatch):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    query = {"trim": TRIM_QUERY, "distinct": DC_QUERY}.get(plan, QUERY)
+    query = QUERIES.get(plan, QUERY)
     stats = {}
     _, exp = oracle.execute(query, _segments(), stats=stats)
     for rank, groups, reached in got:
         assert set(groups) == set(exp), rank
+        # the broker ORs numGroupsLimitReached over servers: every rank reports the oracle's flag
+        assert reached == bool(stats.get("num_groups_limit_reached", False)), (rank, reached, stats)
         if plan == "trim":
             assert stats["num_groups_limit_reached"]
             assert groups == exp, rank
             continue
-        if plan == "distinct":
+        if plan in ("distinct", "distinct_agg"):
             assert groups == exp, rank
             continue
         for k, e in exp.items():

@@ -7,14 +7,17 @@ table and query) through size-independent properties, since the oracle cannot ru
 * per-segment spot checks: the first and last segment through the HIP path equal the CPU oracle;
 * counting identities: COUNT(*) without a filter is 1e9; the COUNTs of a range, of everything below it
   and of everything above it add up to 1e9; the group COUNTs add up to numDocsMatched.
+
+Subset results are merged with the oracle's own AggregationFunction.merge restatement
+(oracle_reduce.merge), not the product's.
 """
 import math
 
 import pytest
 
 import oracle
+from oracle_reduce import merge as merge_partial
 from pinot_amd import datagen
-from pinot_amd.query import merge_partial
 
 pytestmark = pytest.mark.gpu
 
@@ -93,23 +96,52 @@ def test_full_size_spot_segments_vs_oracle(table):
                 assert _close(x, y), (i, k, j, x, y)
 
 
-# ------------------------------------------------------------------ configs[3] at full per-GPU size
 @pytest.mark.timeout(900)
-def test_full_size_highcard_partitioned_vs_atomic_and_linearity(monkeypatch):
+def test_full_size_readme_query_vs_oracle(table):
+    """configs[0]'s own query (README.md:95-100: an 8-day range AND an IN list, SUM(clicks), SUM(impressions)
+    GROUP BY daysSinceEpoch) on the bench table: the 10M-row segments 0 and 99 equal the oracle, and the
+    100-segment result equals the merge of two disjoint subsets."""
+    E, segs, spot = table
+    ex = E.ServerQueryExecutor()
+    q = datagen.README_QUERY
+    for i, bufs in spot.items():
+        got = ex.execute(q, [segs[i]]).groups()
+        _, exp = oracle.execute(q, [bufs])
+        assert len(exp) == 8 and set(got) == set(exp), (i, sorted(got), sorted(exp))
+        for k, e in exp.items():
+            assert got[k] == e, (i, k, got[k], e)  # integer SUMs: exact
+    full = ex.execute(q, segs)
+    g = full.groups()
+    a = ex.execute(q, segs[:61]).groups()
+    for k, v in ex.execute(q, segs[61:]).groups().items():
+        a[k] = [merge_partial(f, x, y) for f, x, y in zip(["SUM", "SUM"], a[k], v)] if k in a else v
+    assert a == g and len(g) == 8
+
+
+# ------------------------------------------------------------------ configs[3] at full per-GPU size
+@pytest.fixture(scope="module")
+def highcard_table():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    from pinot_amd import engine as E
+    segs, spot = [], {}
+    for i in range(NSEG):
+        b = datagen.highcard_segment(f"hc{i}", ROWS, seed=1000 + i)
+        segs.append(E.ImmutableSegment(b))
+        if i in (0, NSEG - 1):
+            spot[i] = b
+        del b
+    return E, segs, spot
+
+
+@pytest.mark.timeout(900)
+def test_full_size_highcard_partitioned_vs_atomic_and_linearity(highcard_table, monkeypatch):
     """configs[3] per GPU: 1B rows in 100 segments, ~1M (dimA, dimB) groups. The partitioned plan
     (count / scatter / LDS-aggregate) must equal the direct HBM-atomic plan group by group (COUNT,
     integer SUM, MIN(LONG), MAX(DOUBLE) are all order-independent, so exactly), the result must be the
     merge of two disjoint segment subsets, and the first segment must equal the oracle."""
-    import torch
-    assert torch.cuda.is_available()
-    from pinot_amd import engine as E
-    segs, spot = [], None
-    for i in range(NSEG):
-        b = datagen.highcard_segment(f"hc{i}", ROWS, seed=1000 + i)
-        segs.append(E.ImmutableSegment(b))
-        if i == 0:
-            spot = b
-        del b
+    E, segs, spots = highcard_table
+    spot = spots[0]
     q = datagen.HIGHCARD_QUERY
     ex = E.ServerQueryExecutor()
     monkeypatch.setenv("PINOT_AMD_PARTITIONED", "1")
@@ -133,6 +165,40 @@ def test_full_size_highcard_partitioned_vs_atomic_and_linearity(monkeypatch):
     got = ex.execute(q, [segs[0]]).groups()
     _, exp = oracle.execute(q, [spot])
     assert got == exp
+
+
+@pytest.mark.timeout(900)
+def test_full_size_highcard_default_limit_vs_oracle(highcard_table, monkeypatch):
+    """configs[3]'s query as Pinot runs it by default (numGroupsLimit 100000 < 1M keys per segment), on the
+    default plan (sequential admission over segment prefixes + partitioned aggregation of admitted docs):
+    segments 0 and 99 equal the oracle's literal first-seen admission (DictionaryBasedGroupKeyGenerator
+    .java:1017-1040) including numGroupsLimitReached; the 100-segment result equals the merge of two
+    disjoint subsets (admission is per segment); segment 0 is the same on the first-doc admission."""
+    E, segs, spots = highcard_table
+    q = datagen.HIGHCARD_DEFAULT_QUERY
+    ex = E.ServerQueryExecutor()
+    full = ex.execute(q, segs)
+    assert "+admit-seq" in full.kernel_info(), full.kernel_info()
+    assert full.num_groups_limit_reached()
+    g_full = full.groups()
+    assert sum(v[0] for v in g_full.values()) < full.num_docs_matched()  # dropped docs were scanned
+    for i, bufs in spots.items():
+        r = ex.execute(q, [segs[i]])
+        stats = {}
+        _, exp = oracle.execute(q, [bufs], stats=stats)
+        assert len(exp) == 100_000
+        assert r.num_groups_limit_reached() == stats["num_groups_limit_reached"] is True
+        assert r.groups() == exp, i
+    funcs = ["COUNT", "SUM", "MIN", "MAX"]
+    a = ex.execute(q, segs[:50]).groups()
+    for k, v in ex.execute(q, segs[50:]).groups().items():
+        a[k] = [merge_partial(f, x, y) for f, x, y in zip(funcs, a[k], v)] if k in a else v
+    assert a == g_full
+    monkeypatch.setenv("PINOT_AMD_ADMIT_SEQ", "0")
+    r = ex.execute(q, [segs[0]])
+    assert "+admit" in r.kernel_info() and "+admit-seq" not in r.kernel_info(), r.kernel_info()
+    _, exp = oracle.execute(q, [spots[0]])
+    assert r.groups() == exp
 
 
 # ------------------------------------------------------------------ configs[4] at full size (SF100)

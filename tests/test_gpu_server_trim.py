@@ -2,7 +2,9 @@
 .createIndexedTableForCombineOperator + IndexedTable.finish) against the oracle's restatement
 (oracle_reduce.server_table): LIMIT groups without ORDER BY; the top max(5 * LIMIT, minServerGroupTrimSize)
 by ORDER BY on group columns and final aggregation values (AVG, MIN, SUM) otherwise; trimming disabled
-with minServerGroupTrimSize <= 0; through the dense and hash plans."""
+with minServerGroupTrimSize <= 0; LIMIT groups under a safe trim (ORDER BY = GROUP BY) below
+sortAggregateLimitThreshold and with serverReturnFinalResult; DISTINCTCOUNT folded before the table;
+through the dense and hash plans; and every SSB query (their ORDER BYs are mostly safe trims)."""
 import numpy as np
 import pytest
 
@@ -24,6 +26,15 @@ QUERIES = [
     "SET minServerGroupTrimSize = 20; SELECT d0, AVG(r_int), MAX(r_double) FROM t GROUP BY d0 "
     "ORDER BY AVG(r_int) LIMIT 5",
     "SET minServerGroupTrimSize = -1; SELECT d1, COUNT(*) FROM t GROUP BY d1 ORDER BY COUNT(*) DESC LIMIT 1",
+    # safe trim (ORDER BY keys = GROUP BY keys): the sorted combine keeps LIMIT groups
+    "SELECT d0, d1, COUNT(*), SUM(r_long) FROM t GROUP BY d0, d1 ORDER BY d1, d0 DESC LIMIT 6",
+    "SET serverReturnFinalResult = true; SELECT d0, SUM(r_long), COUNT(*) FROM t GROUP BY d0 "
+    "ORDER BY SUM(r_long) DESC LIMIT 4",
+    # DISTINCTCOUNT: the value sets are folded first, then the table (round-3 advisor: a LIMIT on the
+    # (group, value) sub-queries cut the sets)
+    "SET minServerGroupTrimSize = 3; SELECT d0, DISTINCTCOUNT(d1), COUNT(*) FROM t GROUP BY d0 "
+    "ORDER BY DISTINCTCOUNT(d1) DESC LIMIT 2",
+    "SELECT d0, DISTINCTCOUNT(d1) FROM t GROUP BY d0 LIMIT 5",
 ]
 
 
@@ -47,3 +58,43 @@ def test_server_table_vs_oracle(qi, plan, monkeypatch):
     assert_same_groups(got, exp, fsum)
     if qc.order_by:  # the table is sorted by the ORDER BY
         assert list(got) == list(exp)
+
+
+def test_segment_level_safe_trim_is_refused(monkeypatch):
+    """LIMIT >= sortAggregateLimitThreshold under a safe trim: each segment would keep only its top LIMIT
+    groups (GroupByOperator.java:146-182); the library refuses rather than returning other groups."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import _lib
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(7)
+    bufs = [random_segment(rng, 20_000, name="sf0", bits_cards=(300, 37))]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY d0 LIMIT 5"
+    with pytest.raises(_lib.PinotAmdError, match="safe trim"):
+        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
+    # no segment can hold more than LIMIT groups: nothing to trim, accepted
+    q2 = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t WHERE d0 < 3 GROUP BY d0 ORDER BY d0 LIMIT 5"
+    got = E.ServerQueryExecutor(server_trim=True).execute(q2, segs).groups()
+    _, full = oracle.execute(q2, bufs)
+    assert got == server_table(parse_sql(q2), full)
+
+
+def test_ssb_server_table_vs_oracle():
+    """Every SSB query with the server's combine table on the device, over segments with different
+    dictionaries, against oracle_reduce.server_table of the oracle's groups."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import engine as E
+    from pinot_amd import ssb
+    bufs = [ssb.lineorder_flat_segment(f"st{i}", 200_003 + i, seed=40 + i) for i in range(3)]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    for name, sql in ssb.SSB_QUERIES:
+        qc = parse_sql(sql)
+        if not qc.group_by:
+            continue
+        got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
+        _, full = oracle.execute(qc, bufs)
+        exp = server_table(qc, full)
+        assert list(got) == list(exp), name
+        assert_same_groups(got, exp, set(range(len(qc.aggregations))))
