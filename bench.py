@@ -16,6 +16,7 @@ Other workloads (one JSON line per query; not the driver's headline line):
   --workload highcard-default  configs[3]'s query at Pinot's default numGroupsLimit (100000 < 1M groups
                         per segment): exact first-seen trimming per segment (sequential admission pass,
                         then the partitioned plan over the admitted docs)
+  --workload wide-keys  5-column GROUP BY past the dense key space: the hash-table plan with its LDS first level
   --workload inverted   configs[2]: inverted-index IN filters, AND/OR over 3 columns, selectivity sweep
   --workload ssb        configs[4]: SSB SF100 denormalized lineorder, Q1.1-Q4.3
 
@@ -60,6 +61,10 @@ def workloads():
                              "configs[3] at Pinot's default numGroupsLimit (100000): GROUP BY on 2 dims (1M keys), "
                              "each segment admits its first 100000 groups (DictionaryBasedGroupKeyGenerator), "
                              "100 segments x 10M rows per GPU", None),
+        "wide-keys": (datagen.widekeys_segment, [datagen.WIDEKEYS_QUERY], datagen.WIDEKEYS_BYTES_PER_ROW,
+                      "wide group keys: GROUP BY 5 dictionary columns (key space 4e18 > the 2^28 dense cap: the "
+                      "hash-table plan, DictionaryBasedGroupKeyGenerator's map-based holders) over 1B rows in 100 "
+                      "segments, ~1M groups of Zipf(1.1)-distributed entities, COUNT / SUM(INT) / MAX(DOUBLE)", None),
         "inverted": (datagen.inverted_segment, [datagen.inverted_query(s) for s in datagen.INVERTED_SELECTIVITIES],
                      None,
                      "configs[2]: inverted-index IN filters combined with AND/OR across 3 columns (10000-value "
@@ -109,7 +114,7 @@ PLAN_KERNELS = {
     "jit-wselect": "pinot_select(word-level)+pinot_gather",
     "jit-fwselect": "roaring_select_kernel (inverted-index expansion + word-level select, one launch)+pinot_gather",
     "jit-partitioned": "pinot_part_scatter+pinot_part_agg (+pinot_part_count, or the direct-atomic pinot_scan_jit on handover)",
-    "jit-hash": "pinot_scan_jit (HBM hash table)",
+    "jit-hash": "pinot_scan_jit (LDS-privatised first level + HBM hash table)",
     "jit-hash-trim": "pinot_scan_jit (HBM hash table keyed by segment) + trim_* + hash_merge_kernel",
 }
 
@@ -163,7 +168,7 @@ def committed_traffic(query: str, kernel_info: str, rows: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="scan", choices=["readme", "scan", "highcard", "highcard-default", "inverted", "ssb"])
+    ap.add_argument("--workload", default="scan", choices=["readme", "scan", "highcard", "highcard-default", "wide-keys", "inverted", "ssb"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default 100; ssb: 60 = SF100)")

@@ -1868,6 +1868,7 @@ static int run_plan(pinot_amd_result* r) {
   unsigned long long* limit_flag = ctr + 3 * nl;
   unsigned long long* overflow = ctr + 3 * nl + 1;
   if (r->kind == PLAN_HASH) {
+   for (;;) {  // untrimmed hash plans: the table grows and the plan runs again while docs found no slot
     HIP_OK(hipMemsetAsync(r->fkeys.p, 0xFF, (size_t)r->nw * (size_t)r->fcap * 8, st));  // EMPTY key words
     HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, r->fcap, st));
     for (int b = 0; b < r->nbatches; ++b) {
@@ -1902,6 +1903,26 @@ static int run_plan(pinot_amd_result* r) {
                                  (uint64_t*)r->acc.p, r->q, r->fd_acc, (const int64_t*)r->t_dstar.p, overflow, st));
       }
     }
+    if (r->trim) break;
+    // The table's capacity comes from a group-count bound (docs per segment, key space); real group counts
+    // are usually far lower, so the plan starts small (PINOT_AMD_HASH_INIT_SLOTS) and, like the map-based
+    // holders that resize as groups arrive, grows 4x when some doc found no slot (then runs again).
+    unsigned long long ovf = 0;
+    HIP_OK(hipMemcpyAsync(&ovf, overflow, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (ovf == 0) break;
+    const int64_t ncap = r->fcap * 4;
+    const double nbytes = (double)ncap * (double)(r->nw + r->q.nacc) * 8.0;
+    if (ncap > ((int64_t)1 << 31) || nbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
+      break;  // the overflow counter stays set: the result reports EOVERFLOW
+    r->fkeys.reset();
+    r->acc.reset();
+    if (int rc = r->fkeys.alloc((size_t)r->nw * (size_t)ncap * 8)) return rc;
+    if (int rc = r->acc.alloc((size_t)r->q.nacc * (size_t)ncap * 8)) return rc;
+    r->fcap = ncap;
+    r->compacted = false;
+    HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
+   }
   } else {
     if (r->admit)
       if (int rc = run_admission(r, limit_flag)) return rc;
@@ -2336,8 +2357,11 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     fbound = std::min(fbound, keyspace);
     const int64_t max_cap = (int64_t)1 << 31;  // compaction indexes slots with int32
     auto bytes_of = [&](int64_t cap, int words) { return (double)cap * (double)(words + nacc) * 8.0; };
-    // the final table holds every admitted group at once (it cannot be batched)
-    const int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)std::min(2.0 * fbound, (double)max_cap)));
+    // the final table holds every admitted group at once (it cannot be batched); untrimmed plans start at
+    // most PINOT_AMD_HASH_INIT_SLOTS slots and grow when groups overflow it (run_plan)
+    double want = std::min(2.0 * fbound, (double)max_cap);
+    if (!r->trim) want = std::min(want, (double)env_i64("PINOT_AMD_HASH_INIT_SLOTS", (int64_t)1 << 24));
+    const int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)want));
     const double fbytes = bytes_of(fcap, r->nw);
     if (fbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
       return fail(PINOT_AMD_EUNSUPPORTED, "group table of %lld slots (%.1f GB) exceeds PINOT_AMD_HASH_FINAL_MAX_BYTES",
@@ -2510,6 +2534,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     return (int64_t)k;
   };
   int64_t lds_bytes = (int64_t)q.nacc * std::max<int64_t>(num_keys, 1) * 8;
+  int64_t hash_lds_bytes = 0;  // hash plans: the LDS first level (JitPlan::hash_lds)
   std::vector<int64_t> part_vbase;  // partitioned plans: integer record fields' bases (DevPartition::vbase)
   if (r->kind == PLAN_DENSE && q.nacc > 0) {
     const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
@@ -2721,6 +2746,26 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
 
+  // Hash-table plans (DictionaryBasedGroupKeyGenerator's map-based holders) get an LDS-privatised first
+  // level: one CU-wide block (4 x 256 threads) per CU keeps up to S keys with their accumulators in LDS,
+  // so repeated keys (skewed group distributions) aggregate on-die and reach the HBM table once per block
+  // instead of once per doc. Not for trimming plans (their keys carry the segment) or selection-vector
+  // gathers. PINOT_AMD_HASH_LDS=0 disables it, PINOT_AMD_HASH_LDS_SLOTS sets S.
+  if (base.hash && !r->trim && !base.select && q.nacc > 0 && !env_is("PINOT_AMD_HASH_LDS", "0")) {
+    const int64_t slot_bytes = (int64_t)(base.hash_words + 1 + (int)base.accs.size()) * 8;
+    int64_t S = env_i64("PINOT_AMD_HASH_LDS_SLOTS", 0);
+    if (S <= 0) {
+      S = 4096;
+      while (S > 64 && S * slot_bytes > std::min<int64_t>(lds_max, 128 * 1024)) S >>= 1;
+    }
+    S = next_pow2(std::max<int64_t>(64, S));
+    if (S * slot_bytes <= lds_max) {
+      base.hash_lds = (int)S;
+      base.scan_nsub = kPartSub;
+      hash_lds_bytes = S * slot_bytes;
+    }
+  }
+
   clk.mark("plan");
   // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
   const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
@@ -2879,12 +2924,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           jl.mask = maxc <= 32 ? 1 : 2;
           jl.bits_regs = 0;
           // fixed-bit columns of <= 6 bits in 256-thread scan / select blocks: an LDS accept table per
-          // (clause, column) indexed by F = 4, 2 or 1 packed fields (4 / F lookups per lane of 4 docs). A
-          // table of <= 2^8 bytes spans <= 64 dwords, one per LDS bank, so a wave's 64 random lookups never
-          // conflict (lanes reading one dword broadcast); larger tables (the round-3 4-field tables of 3-bit
-          // columns: 4 KiB) cost ~6 conflict cycles per lookup (pmc_ssb11). PINOT_AMD_LUT_MAX_BITS raises the cap.
+          // (clause, column) indexed by F = 4, 2 or 1 packed fields (4 / F lookups per lane of 4 docs), the
+          // table at most 2^PINOT_AMD_LUT_MAX_BITS bytes (default 12: 4 KiB, one lookup per 4 docs for <= 3
+          // bits). Tables of <= 2^8 bytes (one dword per LDS bank) never conflict, but the extra lookups
+          // cost more than the ~6 conflict cycles they save: SSB 8.50 -> 8.56 ms at a 2^8 cap
+          // (profiles/r04/sweep_ssb_lut_cap.txt) -- the select pass is latency-bound, not LDS-bound.
           const JitSlot& js = jp.slots[jl.slot];
-          static const int lut_max = (int)std::min<int64_t>(12, std::max<int64_t>(6, env_i64("PINOT_AMD_LUT_MAX_BITS", 8)));
+          static const int lut_max = (int)std::min<int64_t>(12, std::max<int64_t>(6, env_i64("PINOT_AMD_LUT_MAX_BITS", 12)));
           if (js.enc == ENC_FIXED_BIT && js.bits >= 1 && js.bits <= 6 && !jp.partitioned &&
               (jp.scan_nsub == 1 || jp.select) && !env_is("PINOT_AMD_LEAF_LUT", "0"))
             jl.lut = 4 * js.bits <= lut_max ? 4 * js.bits : 2 * js.bits <= lut_max ? 2 * js.bits : js.bits;
@@ -3000,7 +3046,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.fd_full_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, tiles));
     }
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
-    L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : 0;
+    L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : jp.hash_lds ? (size_t)hash_lds_bytes : 0;
     for (const JitLeaf& jl : jp.leaves) L.shmem_sets += (size_t)jl.lds_words * 4;
     {  // LDS accept tables: one per (clause, column) mask group with a lookup table (jit.cpp's layout)
       std::vector<std::pair<int, int>> groups;

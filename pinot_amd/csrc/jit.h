@@ -14,6 +14,7 @@ constexpr int kPartSub = 4;  // partition count / scatter blocks: 4 x 256 thread
 constexpr int kPartCountRatio = 2;  // count-pass blocks per scatter-pass block (count needs little LDS)
 constexpr int64_t kAdmitSeqMaxKeys = 1 << 20;  // sequential admission: the seen-key bitmap (128 KiB) in LDS
 constexpr int kAdmitSeqSlots = 2048;           // its per-tile hash table of new keys (key, first doc)
+constexpr int kHashLdsProbes = 8;              // LDS first level of a hash plan: slots probed before HBM
 // LDS bytes of the sequential admission kernel for a key space
 inline size_t jit_admitseq_lds(int64_t num_keys) {
   return (size_t)((num_keys + 31) / 32) * 4 + kAdmitSeqSlots * 8 + 1024 * 4 + 80 * 4;
@@ -110,6 +111,11 @@ struct JitPlan {
   int hash_words = 0;          // key words including the segment word
   bool hash_seg = false;
   std::vector<std::pair<int, int>> hash_pack;
+  // > 0: an LDS-privatised first level of hash_lds slots (a power of two) in front of the HBM table: a
+  // doc's key is probed in the block's LDS table first (linear probing, <= kHashLdsProbes slots); only a
+  // key that finds no LDS slot goes to the HBM table directly; the block flushes its occupied slots into
+  // the HBM table at the end (one HBM probe + one atomic per accumulator per slot)
+  int hash_lds = 0;
   // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;

@@ -121,6 +121,51 @@ HIGHCARD_BYTES_PER_ROW =2 * S.num_bits_per_value(HC_CARD - 1) / 8.0 + 4 + 8 + 8
 
 
 # ---------------------------------------------------------------------------------------------
+# Wide group keys (the map-based holders of DictionaryBasedGroupKeyGenerator.java:444-900): a 5-column
+# GROUP BY whose key space (20000^3 x 1000 x 500 = 4e18, 64 bits: two packed key words) is far past the
+# dense cap (2^28), so the hash-table plan runs. Rows belong to ~1M entities drawn Zipf(1.1) (a few
+# entities hold most rows, as real dimension data does); each entity's 5 attributes are fixed functions of
+# it, so the present groups number ~1M although the key space is astronomically larger.
+WIDE_ENTITIES = 1 << 20
+WIDE_CARDS = (20000, 20000, 20000, 1000, 500)
+WIDE_COLUMNS = ("w1", "w2", "w3", "w4", "w5")
+_WIDE_MUL = (2654435761, 2246822519, 3266489917, 668265263, 374761393)
+
+
+def widekeys_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+    """Segment of the wide-key table: entity e ~ Zipf(1.1) over WIDE_ENTITIES ranks (inverse-CDF of the
+    continuous Pareto approximation), dimension j = (e * m_j + j) mod card_j as a fixed-bit dictionary column
+    (the first card_j docs take every dictionary value once), raw INT / DOUBLE metrics."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = num_docs
+    u = torch.rand((n,), generator=g, device=device, dtype=torch.float64)
+    s_ = 1.1
+    a = WIDE_ENTITIES ** (1.0 - s_)
+    ent = torch.clamp(((a - 1.0) * u + 1.0) ** (1.0 / (1.0 - s_)), 1.0, float(WIDE_ENTITIES)).to(torch.int64) - 1
+    cols = {}
+    for j, (cname, card) in enumerate(zip(WIDE_COLUMNS, WIDE_CARDS)):
+        ids = ((ent * _WIDE_MUL[j] + j) % card).to(torch.int32)
+        ids[:card] = torch.arange(card, device=device, dtype=torch.int32)
+        bits = S.num_bits_per_value(card - 1)
+        dvals = np.arange(card, dtype=np.int32)
+        cols[cname] = S.ColumnBuffers(cname, S.INT, n, True, False, card, bits, _fixed_bit(ids, bits),
+                                      S.dictionary_bytes(dvals, S.INT), None, dvals)
+    met_int = torch.randint(0, 1000, (n,), generator=g, device=device, dtype=torch.int32)
+    met_double = torch.randn((n,), generator=g, device=device, dtype=torch.float64) * 1000.0
+    for cname, t, st, size in (("metInt", met_int, S.INT, 4), ("metDouble", met_double, S.DOUBLE, 8)):
+        cols[cname] = S.ColumnBuffers(cname, st, n, False, fwd=S.raw_fwd_header(n, st) + _be_bytes(t, size))
+    torch.cuda.synchronize()
+    return S.SegmentBuffers(name, n, cols)
+
+
+WIDEKEYS_QUERY = ("SET numGroupsLimit = 2000000000; SELECT w1, w2, w3, w4, w5, COUNT(*), SUM(metInt), MAX(metDouble) "
+                  "FROM wide WHERE metInt < 900 GROUP BY w1, w2, w3, w4, w5")
+WIDEKEYS_BYTES_PER_ROW = sum(S.num_bits_per_value(c - 1) for c in WIDE_CARDS) / 8.0 + 4 + 8
+
+
+# ---------------------------------------------------------------------------------------------
 # BASELINE.json configs[2]: inverted-index EQ/IN filters combined with AND/OR across 3 columns
 INV_CARD = 10000           # dictionary cardinality of invA / invB / invC (14-bit fixed-bit forward index)
 INV_COLUMNS = ("invA", "invB", "invC")

@@ -115,7 +115,11 @@ def test_full_size_readme_query_vs_oracle(table):
     a = ex.execute(q, segs[:61]).groups()
     for k, v in ex.execute(q, segs[61:]).groups().items():
         a[k] = [merge_partial(f, x, y) for f, x, y in zip(["SUM", "SUM"], a[k], v)] if k in a else v
-    assert a == g and len(g) == 8
+    # SUM(impressions) passes 2^53: each subset's exact sum is rounded once, so their double merge may differ
+    # from the whole table's by an ulp (the 1e-12 relative bound of north_star)
+    assert set(a) == set(g) and len(g) == 8
+    for k in g:
+        assert all(_close(x, y) for x, y in zip(g[k], a[k])), (k, g[k], a[k])
 
 
 # ------------------------------------------------------------------ configs[3] at full per-GPU size
