@@ -154,7 +154,8 @@ struct ChunkJob {
 struct DevHash {
   unsigned long long* keys;
   int64_t cap;                       // power of two
-  unsigned long long* overflow;      // docs that found no free slot (the host fails the query if > 0)
+  unsigned long long* overflow;      // docs that found no free slot (the host grows the table or fails)
+  int64_t max_probe;                 // > 0: a key gives up after this many slots (linear probing), 0: cap
 };
 
 // Group keys by value for the cross-rank merge (the broker reduce on the device): group column j's

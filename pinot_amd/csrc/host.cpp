@@ -1884,6 +1884,9 @@ static int run_plan(pinot_amd_result* r) {
       } else {
         H.keys = (unsigned long long*)r->fkeys.p;
         H.cap = r->fcap;
+        // a probe chain this long means a crowded table: the doc counts as overflow and the table grows
+        // (below) instead of degrading into long serial CAS walks
+        H.max_probe = env_i64("PINOT_AMD_HASH_MAX_PROBE", 512);
         table = (uint64_t*)r->acc.p;
       }
       H.overflow = overflow;
@@ -2360,7 +2363,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     // the final table holds every admitted group at once (it cannot be batched); untrimmed plans start at
     // most PINOT_AMD_HASH_INIT_SLOTS slots and grow when groups overflow it (run_plan)
     double want = std::min(2.0 * fbound, (double)max_cap);
-    if (!r->trim) want = std::min(want, (double)env_i64("PINOT_AMD_HASH_INIT_SLOTS", (int64_t)1 << 24));
+    if (!r->trim) want = std::min(want, (double)env_i64("PINOT_AMD_HASH_INIT_SLOTS", (int64_t)1 << 20));
     const int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)want));
     const double fbytes = bytes_of(fcap, r->nw);
     if (fbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
@@ -2752,17 +2755,22 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   // instead of once per doc. Not for trimming plans (their keys carry the segment) or selection-vector
   // gathers. PINOT_AMD_HASH_LDS=0 disables it, PINOT_AMD_HASH_LDS_SLOTS sets S.
   if (base.hash && !r->trim && !base.select && q.nacc > 0 && !env_is("PINOT_AMD_HASH_LDS", "0")) {
-    const int64_t slot_bytes = (int64_t)(base.hash_words + 1 + (int)base.accs.size()) * 8;
+    // integer SUMs in the LDS level keep int64 partials (no high-word array) when a CU-wide block's docs x
+    // |value| fit (the HBM path of the same kernel always adds 128 bits); the grid has >= min(CUs, tiles / 4)
+    // blocks
+    const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
+    set_narrow((__int128)((all_tiles + min_grid - 1) / min_grid) * kTileDocs);
+    const int64_t slot_bytes = (int64_t)(base.hash_words + lds_arrays()) * 8;
+    // as many slots as the LDS holds beside the kernel's static LDS (counters), a multiple of 64
     int64_t S = env_i64("PINOT_AMD_HASH_LDS_SLOTS", 0);
-    if (S <= 0) {
-      S = 4096;
-      while (S > 64 && S * slot_bytes > std::min<int64_t>(lds_max, 128 * 1024)) S >>= 1;
-    }
-    S = next_pow2(std::max<int64_t>(64, S));
-    if (S * slot_bytes <= lds_max) {
+    if (S <= 0) S = std::min<int64_t>(8192, (lds_max - 1024) / slot_bytes);
+    S = std::max<int64_t>(64, S / 64 * 64);
+    if (S * slot_bytes <= lds_max - 1024) {
       base.hash_lds = (int)S;
       base.scan_nsub = kPartSub;
       hash_lds_bytes = S * slot_bytes;
+    } else {
+      for (JitAcc& a : base.accs) a.narrow = 0;
     }
   }
 
@@ -2982,6 +2990,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
       jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
       jp.flush_every = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_EVERY", 1)));
+      jp.flush_par = !env_is("PINOT_AMD_FLUSH_PAR", "0");
     }
     {  // algorithmic bytes: each decoded column once (fixed-bit at its width, raw at its value width)
       for (size_t k = 0; k < L.segs.size(); ++k)

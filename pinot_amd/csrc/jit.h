@@ -99,6 +99,10 @@ struct JitPlan {
   int stage_cap = 0;           // scatter: records staged per partition in LDS (0: direct writes)
   int flush_pct = 85;          // scatter: a partition is written out once this % of its staging is filled (swept: 85 best)
   int flush_every = 1;         // scatter: the staged partitions are checked (two block barriers) every n tile steps
+  // scatter: the wave's ready partitions are written out lane-parallel (their runs concatenated, each lane
+  // one 16 / 8 B unit, owners found by a binary search over the lanes' prefix sums) instead of one run
+  // after another with the whole wave on each run
+  bool flush_par = true;
   // Sampled capacities instead of the exact count pass: a histogram over every sample_stride-th tile
   // sizes each partition's region (DevPartition::cap); the scatter reserves space with one global
   // atomic per flushed run, records beyond a region's capacity go to the overflow slab, aggregated
@@ -111,7 +115,7 @@ struct JitPlan {
   int hash_words = 0;          // key words including the segment word
   bool hash_seg = false;
   std::vector<std::pair<int, int>> hash_pack;
-  // > 0: an LDS-privatised first level of hash_lds slots (a power of two) in front of the HBM table: a
+  // > 0: an LDS-privatised first level of hash_lds slots (a multiple of 64) in front of the HBM table: a
   // doc's key is probed in the block's LDS table first (linear probing, <= kHashLdsProbes slots); only a
   // key that finds no LDS slot goes to the HBM table directly; the block flushes its occupied slots into
   // the HBM table at the end (one HBM probe + one atomic per accumulator per slot)
