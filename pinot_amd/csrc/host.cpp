@@ -1142,7 +1142,7 @@ struct Launch {
   JitKernel* jit = nullptr;         // scan, or the partitioned count / scatter / aggregate trio
   JitKernel* jit_atomic = nullptr;  // partitioned: direct-atomic scan used when few docs match
   JitKernel* jit_sample = nullptr;  // partitioned: match count over every sample_stride-th tile
-  int grid = 1, atomic_grid = 1, sample_grid = 1, agg_grid = 1, scan_nsub = 1;
+  int grid = 1, atomic_grid = 1, sample_grid = 1, agg_grid = 1, scan_nsub = 1, part_sub = kPartSub;
   size_t shmem = 0, shmem_scatter = 0, shmem_agg = 0;
   DevPartition part{};
   int64_t docs = 0, tiles = 0;
@@ -1710,7 +1710,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
                                  nullptr));
     return 0;
   }
-  const unsigned pt = (unsigned)(kBlock * kPartSub);
+  const unsigned pt = (unsigned)(kBlock * L.part_sub);
   const unsigned count_grid = (unsigned)(L.grid * kPartCountRatio);
   if (L.part_sampled) {
     // per scatter block: strided histogram -> allotments -> (direct-atomic scan | scatter) -> records
@@ -2984,8 +2984,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (jp.part_sampled) L.part.sample_stride = stride;
       // scatter staging: as many records per partition as the LDS holds (up to 64); below 4 a run is
       // too short to pay for the staging round trip and records are written directly
+      // PINOT_AMD_PART_SUB: 256-thread groups per scatter block (4: one CU-wide block per CU, 2 / 1: two / four
+      // blocks per CU sharing the LDS)
+      jp.part_sub = (int)env_i64("PINOT_AMD_PART_SUB", kPartSub);
+      if (jp.part_sub != 1 && jp.part_sub != 2) jp.part_sub = kPartSub;
+      const size_t stage_lds = (size_t)lds_max / (size_t)(kPartSub / jp.part_sub);
       int cap = 64;
-      while (cap >= 4 && jit_scatter_lds(jp, cap) > (size_t)lds_max) --cap;
+      while (cap >= 4 && jit_scatter_lds(jp, cap) > stage_lds) --cap;
       jp.stage_cap = cap >= 4 ? cap : 0;
       if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
       jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
@@ -3114,7 +3119,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         max_slab_docs = std::max(max_slab_docs, (size_t)L.docs + 64);
       }
       int nb = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn_scatter, kBlock * kPartSub, L.shmem_scatter) !=
+      L.part_sub = jp.part_sub;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn_scatter, kBlock * jp.part_sub, L.shmem_scatter) !=
               hipSuccess || nb < 1)
         nb = 1;
       per_cu = nb;
@@ -3187,7 +3193,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     // persistent grid: resident blocks per CU x CUs (a larger grid would only queue a tail)
     int64_t grid = (int64_t)cus * per_cu;
     if (grid > tiles) grid = std::max<int64_t>(tiles, 1);
-    if ((jp.partitioned || L.scan_nsub > 1) && grid * kPartSub > tiles) grid = std::max<int64_t>((tiles + kPartSub - 1) / kPartSub, 1);
+    {
+      const int sub = jp.partitioned ? jp.part_sub : L.scan_nsub;  // tiles a block takes per step
+      if (sub > 1 && grid * sub > tiles) grid = std::max<int64_t>((tiles + sub - 1) / sub, 1);
+    }
     if (L.part_sampled) {  // allotment tables of <= 2 x CUs scatter blocks sit behind the aggregation table
       grid = std::min<int64_t>(grid, 2 * (int64_t)cus);
       L.shmem_agg += (size_t)(2 * grid + 1) * 8;

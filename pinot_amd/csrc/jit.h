@@ -103,6 +103,9 @@ struct JitPlan {
   // one 16 / 8 B unit, owners found by a binary search over the lanes' prefix sums) instead of one run
   // after another with the whole wave on each run
   bool flush_par = true;
+  // partitioned plans: 256-thread groups per count / scatter block (4: one CU-wide block per CU with all the
+  // LDS for staging; 2 / 1: two / four blocks per CU, each with that share of the LDS)
+  int part_sub = kPartSub;
   // Sampled capacities instead of the exact count pass: a histogram over every sample_stride-th tile
   // sizes each partition's region (DevPartition::cap); the scatter reserves space with one global
   // atomic per flushed run, records beyond a region's capacity go to the overflow slab, aggregated
