@@ -106,6 +106,7 @@ struct JitPlan {
   // partitioned plans: 256-thread groups per count / scatter block (4: one CU-wide block per CU with all the
   // LDS for staging; 2 / 1: two / four blocks per CU, each with that share of the LDS)
   int part_sub = kPartSub;
+  bool scatter_batch = true;  // scatter: a lane's staging-slot atomics issued together (PINOT_AMD_SCATTER_BATCH=0: one by one)
   // Sampled capacities instead of the exact count pass: a histogram over every sample_stride-th tile
   // sizes each partition's region (DevPartition::cap); the scatter reserves space with one global
   // atomic per flushed run, records beyond a region's capacity go to the overflow slab, aggregated

@@ -14,10 +14,12 @@ OUT=gpurun_out/prof_$ROUND
 mkdir -p $OUT
 args_for() {
   case $1 in
+    readme) echo "--workload readme --segments 1" ;;
     scan) echo "--segments 40" ;;
     highcard) echo "--workload highcard --segments 40" ;;
     hcdef) echo "--workload highcard-default --segments 40" ;;
     widekeys) echo "--workload wide-keys --segments 40" ;;
+    inv1[0-9]) echo "--workload inverted --segments 40 --query-index ${1#inv}" ;;
     inv[0-9]) echo "--workload inverted --segments 40 --query-index ${1#inv}" ;;
     ssb[0-9]|ssb1[0-2]) echo "--workload ssb --segments 20 --query-index ${1#ssb}" ;;
   esac
