@@ -42,7 +42,7 @@ for w in ${WORKLOADS:-scan highcard hcdef}; do
     timeout -s KILL 150 rocprofv3 --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py $A --steps 3 --warmup 1 > $D/pmc$i.json 2> $D/pmc$i.err || { echo "$w pmc$i failed"; tail -5 $D/pmc$i.err; exit 1; }
     echo "$w pmc$i done"
   done
+  # summarise this workload on the box and drop its raw traces (gpurun copies back at most 64 MiB)
+  COMMIT=${COMMIT:-unknown} python3 profiles/summarize.py --one $OUT gpurun_out/prof_${ROUND}_summary $w > /dev/null || { echo "$w summary failed"; exit 1; }
+  find $D -name "run_kernel_trace.csv" -o -name "run_counter_collection.csv" | xargs rm -f
 done
-# summarise on the box and drop the raw traces (gpurun copies back at most 64 MiB)
-COMMIT=${COMMIT:-unknown} python3 profiles/summarize.py $OUT gpurun_out/prof_${ROUND}_summary > /dev/null && \
-  find $OUT -name "run_kernel_trace.csv" -o -name "run_counter_collection.csv" | xargs rm -f

@@ -34,14 +34,16 @@ def bench_line(path):
     return json.loads(lines[-1]) if lines else None
 
 
-def main(src, dst):
+def main(src, dst, only=None):
     os.makedirs(dst, exist_ok=True)
     index = {}
     for w in sorted(os.listdir(src)):
+        if only is not None and w != only:
+            continue
         d = os.path.join(src, w)
         st = os.path.join(d, "trace", "run_kernel_stats.csv")
-        if not os.path.exists(st):
-            continue
+        if not os.path.exists(st) or not os.path.exists(os.path.join(d, "trace", "run_kernel_trace.csv")):
+            continue  # not profiled, or already summarised (raw traces dropped)
         shutil.copy(st, os.path.join(dst, f"kernel_stats_{w}.csv"))
         out = {"workload": w, "kernels": {}}
         tb = bench_line(os.path.join(d, "trace_bench.json"))
@@ -119,5 +121,7 @@ def build_index(dst):
 if __name__ == "__main__":
     if sys.argv[1] == "--index":
         build_index(sys.argv[2])
+    elif sys.argv[1] == "--one":  # one workload: --one <src> <dst> <workload>
+        main(sys.argv[2], sys.argv[3], only=sys.argv[4])
     else:
         main(sys.argv[1], sys.argv[2])
