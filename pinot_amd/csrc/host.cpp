@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -238,6 +239,8 @@ struct Column {
 struct pinot_amd_segment {
   std::string name;
   int64_t num_docs = 0;
+  uint64_t uid = 0;  // process-unique (never reused): keys host-side caches over segment sets
+  uint64_t gen = 0;  // bumped whenever a column is added (a derived dictionary twin included)
   std::map<std::string, std::unique_ptr<Column>> cols;
   int64_t device_bytes = 0;
   // docs matching a filter (signature of its predicates -> count), counted once by the planner's
@@ -668,6 +671,8 @@ int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segme
   auto* s = new pinot_amd_segment();
   s->name = name ? name : "";
   s->num_docs = num_docs;
+  static std::atomic<uint64_t> next_uid{1};
+  s->uid = next_uid.fetch_add(1);
   *out = s;
   return 0;
 }
@@ -689,6 +694,7 @@ const void* pinot_amd_segment_column_fwd(const pinot_amd_segment* seg, const cha
 int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_spec* spec) {
   if (!seg || !spec || !spec->name) return fail(PINOT_AMD_EINVAL, "add_column: bad arguments");
   if (seg->cols.count(spec->name)) return fail(PINOT_AMD_EINVAL, "add_column: duplicate column %s", spec->name);
+  ++seg->gen;
   if (spec->encoding == ENC_RAW && spec->stored_type == T_STRING) {
     // Raw STRING column: staged dictionary-encoded, as ForwardIndexHandler's ENABLE_DICTIONARY operation
     // rewrites it on load (segment/index/loader/ForwardIndexHandler.java): the distinct values sorted in
@@ -1640,8 +1646,36 @@ static int derive_raw_group_dictionary(pinot_amd_segment* s, const std::string& 
   return pinot_amd_segment_add_column(s, &spec);
 }
 
+static int build_merged_keys_uncached(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
+                                      MergedKeyColumn* out);
+
+// Merged dictionaries of a group-by column over a segment set, cached per (column, segments): segments are
+// immutable, and every query grouping by the column over the same batch merges the same dictionaries (SSB
+// Q2.x: 60 dictionaries of 1000 brands, ~5 ms per query).
+static std::mutex g_keys_mu;
+static std::map<std::string, std::shared_ptr<const MergedKeyColumn>> g_keys_cache;
+
 static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
                              MergedKeyColumn* out) {
+  std::string key = col + "|";
+  for (auto* sg : segs) key += std::to_string(sg->uid) + "." + std::to_string(sg->gen) + ",";
+  {
+    std::lock_guard<std::mutex> g(g_keys_mu);
+    auto it = g_keys_cache.find(key);
+    if (it != g_keys_cache.end()) {
+      *out = *it->second;
+      return 0;
+    }
+  }
+  if (int rc = build_merged_keys_uncached(segs, col, out)) return rc;
+  std::lock_guard<std::mutex> g(g_keys_mu);
+  if (g_keys_cache.size() >= 256) g_keys_cache.clear();  // bounded: a server's working set of batches
+  g_keys_cache[key] = std::make_shared<const MergedKeyColumn>(*out);
+  return 0;
+}
+
+static int build_merged_keys_uncached(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
+                                      MergedKeyColumn* out) {
   const Column* c0 = segs[0]->cols.at(col).get();
   out->type = c0->type;
   for (auto* s : segs) {
