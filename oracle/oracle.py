@@ -1,7 +1,8 @@
 """ctypes driver of the CPU oracle (libpinot_oracle.so). TEST INFRASTRUCTURE ONLY.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module; the
-product path (pinot_amd/) never imports it.
+product path (pinot_amd/) never imports it, and it imports nothing of the product: SQL text is compiled by
+oracle_sql.py, segment byte formats are parsed here and in pinot_oracle.c.
 
 The predicate resolution below is an independent Python restatement of
 pinot-core/.../operator/filter/predicate/PredicateEvaluatorProvider.java and the factories it
@@ -22,7 +23,7 @@ import numpy as np
 
 import dataclasses
 
-from pinot_amd.query import Aggregation, QueryContext, parse_sql  # the SQL front end only: no arithmetic
+from oracle_sql import OAgg as Aggregation, OQuery as QueryContext, parse as _parse_sql  # the oracle's own SQL front end
 from oracle_reduce import JDouble, identity_key, java_identity, merge
 from oracle_reduce import rows as reduce_rows
 
@@ -487,6 +488,15 @@ class OracleSegment:
         return tuple(out)
 
 
+def parse_sql(query) -> QueryContext:
+    """The oracle compiles SQL text itself (oracle_sql); an already compiled oracle query passes through."""
+    if isinstance(query, str):
+        return _parse_sql(query)
+    if isinstance(query, QueryContext):
+        return query
+    raise TypeError("the oracle takes SQL text (it does not read the product's QueryContext)")
+
+
 def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True, stats: dict = None,
             literal_int_sum: bool = False):
     """Run a query over segments on the CPU oracle: returns (num_docs_matched, groups) where groups
@@ -495,7 +505,7 @@ def execute(query, segments: Sequence[SegmentBuffers], use_inverted: bool = True
     stats, when given, receives 'num_groups_limit_reached' (any segment's GroupByOperator flag).
     literal_int_sum: integer SUMs accumulate in double in doc order and merge as doubles in segment
     order, the reference's own arithmetic (SumAggregationFunction); default: exact, rounded once."""
-    qc = parse_sql(query) if isinstance(query, str) else query
+    qc = parse_sql(query)
     if literal_int_sum:
         lib().oracle_set_literal_int_sum(1)
         try:
@@ -585,7 +595,7 @@ def cpu_plan(query, seg: SegmentBuffers, use_inverted: bool = True):
     DefaultGroupByExecutor) in pinot_oracle.c and returns the matched-doc count. Predicate resolution,
     buffer setup and the Python conversion of the groups stay outside, so bench.py's cpu_baseline
     times what a Pinot server does per doc and per segment, not this module's Python."""
-    qc = parse_sql(query) if isinstance(query, str) else query
+    qc = parse_sql(query)
     assert not any(a.func == "DISTINCTCOUNT" for a in qc.aggregations), "cpu_plan: no DISTINCTCOUNT"
     os_ = OracleSegment(seg)
     n = seg.num_docs
@@ -730,6 +740,6 @@ def _parts(qc, slots, nat, vals, vali, valh, int_sum):
 
 
 def rows(query, segments, use_inverted: bool = True):
-    qc = parse_sql(query) if isinstance(query, str) else query
+    qc = parse_sql(query)
     _, groups = execute(qc, segments, use_inverted)
     return reduce_rows(qc, groups)

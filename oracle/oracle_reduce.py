@@ -17,8 +17,8 @@ oracle's cross-segment combine and its final rows do not share code with what th
 * Value identity of group keys and DISTINCTCOUNT elements: Double.doubleToLongBits /
   Float.floatToIntBits (every NaN one value, -0.0 != 0.0), as the fastutil maps and sets compare.
 
-Only the SQL parser (pinot_amd.query.parse_sql: text -> QueryContext) is shared with the product; it
-does no arithmetic.
+Queries come from the oracle's own SQL front end (oracle_sql.parse); nothing here imports product code
+(the functions read a compiled query's attributes only).
 """
 from __future__ import annotations
 

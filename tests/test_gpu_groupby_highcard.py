@@ -51,7 +51,7 @@ def test_highcard_partitioned_vs_oracle(engine, qi, n, monkeypatch):
     res = engine.ServerQueryExecutor().execute(qc, [seg])
     # a 1-doc segment has 1-entry dictionaries: its key space fits the LDS table
     assert res.kernel_info() == ("jit-partitioned" if n > 1 else "jit"), res.kernel_info()
-    nm, og = oracle.execute(qc, [bufs])
+    nm, og = oracle.execute("SET numGroupsLimit = 2000000; " + HC_QUERIES[qi], [bufs])
     assert res.num_docs_matched() == nm
     assert not res.num_groups_limit_reached()
     assert_same_groups(res.groups(), og, _fsum(qc))

@@ -70,7 +70,7 @@ def test_packed_records_vs_oracle(engine, monkeypatch, qi):
     qc = parse_sql("SET numGroupsLimit = 2000000; " + QUERIES[qi])
     res = engine.ServerQueryExecutor().execute(qc, segs)
     assert res.kernel_info().startswith("jit-partitioned"), res.kernel_info()
-    nm, og = oracle.execute(qc, bufs)
+    nm, og = oracle.execute("SET numGroupsLimit = 2000000; " + QUERIES[qi], bufs)
     assert res.num_docs_matched() == nm
     fs = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column in ("dbl", "f")}
     assert_same_groups(res.groups(), og, fs)
@@ -106,7 +106,7 @@ def test_sampled_capacities_vs_oracle(engine, monkeypatch, scale, stage_cap, whe
     qc = parse_sql(q)
     res = engine.ServerQueryExecutor().execute(qc, segs)
     assert res.kernel_info().startswith("jit-partitioned"), res.kernel_info()
-    nm, og = oracle.execute(qc, bufs)
+    nm, og = oracle.execute(q, bufs)
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og, {4})
     res.execute_again()  # cursors and the slab reset per execution

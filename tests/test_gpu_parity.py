@@ -247,7 +247,7 @@ def test_random_queries_vs_oracle(engine, qi, n, kernel_mode):
     for inv in (True, False):
         res = engine.ServerQueryExecutor(inv).execute(qc, [seg])
         check_mode(res, kernel_mode)
-        nm, og = oracle.execute(qc, [bufs], inv)
+        nm, og = oracle.execute(q, [bufs], inv)
         assert res.num_docs_matched() == nm
         got = res.groups()
         if not qc.group_by and nm == 0:

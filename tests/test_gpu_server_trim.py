@@ -51,8 +51,8 @@ def test_server_table_vs_oracle(qi, plan, monkeypatch):
     segs = [E.ImmutableSegment(b) for b in bufs]
     qc = parse_sql(QUERIES[qi])
     got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
-    _, full = oracle.execute(qc, bufs)
-    exp = server_table(qc, full)
+    _, full = oracle.execute(QUERIES[qi], bufs)
+    exp = server_table(oracle.parse_sql(QUERIES[qi]), full)
     assert len(got) == len(exp) <= len(full)
     fsum = {i for i, a in enumerate(qc.aggregations) if a.func in ("SUM", "AVG") and a.column == "r_double"}
     assert_same_groups(got, exp, fsum)
@@ -77,7 +77,7 @@ def test_segment_level_safe_trim_is_refused(monkeypatch):
     q2 = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t WHERE d0 < 3 GROUP BY d0 ORDER BY d0 LIMIT 5"
     got = E.ServerQueryExecutor(server_trim=True).execute(q2, segs).groups()
     _, full = oracle.execute(q2, bufs)
-    assert got == server_table(parse_sql(q2), full)
+    assert got == server_table(oracle.parse_sql(q2), full)
 
 
 def test_ssb_server_table_vs_oracle():
@@ -94,7 +94,7 @@ def test_ssb_server_table_vs_oracle():
         if not qc.group_by:
             continue
         got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
-        _, full = oracle.execute(qc, bufs)
-        exp = server_table(qc, full)
+        _, full = oracle.execute(sql, bufs)
+        exp = server_table(oracle.parse_sql(sql), full)
         assert list(got) == list(exp), name
         assert_same_groups(got, exp, set(range(len(qc.aggregations))))

@@ -57,5 +57,5 @@ def test_string_key_order_in_server_table():
     q = "SELECT s, COUNT(*) FROM t GROUP BY s ORDER BY s DESC LIMIT 6"
     got = E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
     _, full = oracle.execute(q, bufs)
-    exp = server_table(parse_sql(q), full)
+    exp = server_table(oracle.parse_sql(q), full)
     assert list(got) == list(exp) and got == exp

@@ -45,7 +45,7 @@ def _check(engine, q, bufs, segs, expect_trim=None):
     qc = parse_sql(q)
     res = engine.ServerQueryExecutor().execute(qc, segs)
     stats = {}
-    nm, og = oracle.execute(qc, bufs, stats=stats)
+    nm, og = oracle.execute(q, bufs, stats=stats)
     if expect_trim is not None:
         info = res.kernel_info()
         assert ("trim" in info or "admit" in info) == expect_trim, info
@@ -240,7 +240,7 @@ def test_mixed_encodings_across_segments(engine):
         qc = parse_sql(q)
         res = engine.ServerQueryExecutor().execute(qc, segs)
         assert " x" in res.kernel_info(), res.kernel_info()  # several launches
-        nm, og = oracle.execute(qc, bufs)
+        nm, og = oracle.execute(q, bufs)
         assert res.num_docs_matched() == nm
         fs = {i for i, a in enumerate(qc.aggregations) if a.func == "SUM" and a.column == "f"}
         assert_same_groups(res.groups(), og, fs)

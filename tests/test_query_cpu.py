@@ -30,7 +30,7 @@ def test_server_table_restatement():
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     from oracle_reduce import server_table
-    from pinot_amd.query import parse_sql
+    from oracle_sql import parse as parse_sql
     groups = {(k % 5, k // 5): [k, float(100 - k)] for k in range(40)}
     qc = parse_sql("SELECT a, b, COUNT(*), SUM(x) FROM t GROUP BY a, b LIMIT 3")
     kept = server_table(qc, groups)
