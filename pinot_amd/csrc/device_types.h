@@ -15,8 +15,9 @@ constexpr int kMaxAcc = 16;                         // accumulator arrays (acc 0
 constexpr int kMaxGroupCols = 16;
 constexpr int kMaxKeyWords = 8;                     // 64-bit words of a hash-table group key
 // slack the kernels may read past the end of a column buffer (5 dwords of a bit window, a 32 B
-// value vector of the last tile)
-constexpr int kPadBytes = kTileDocs * 8 + 256;
+// value vector of the last tile, and up to 3 whole padding tiles of 8-byte values behind a segment's last
+// tile: the tile-level select walks steps of up to 4 tiles of one segment)
+constexpr int kPadBytes = 4 * kTileDocs * 8 + 256;
 
 // column encodings (pinot_amd_fwd_encoding)
 enum : int32_t { ENC_FIXED_BIT = 0, ENC_RAW = 1, ENC_SORTED = 2 };

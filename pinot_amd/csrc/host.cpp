@@ -2782,6 +2782,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         for (JitAcc& a : base.accs) a.narrow = 0;  // HBM tables take full 128-bit adds
       }
     }
+    // tile-level select: 1024-doc tiles per loop step (PINOT_AMD_SEL_GROUP 1 / 2 / 4); the launches'
+    // segment tile ranges are padded to multiples of it below
+    if (base.select && !base.word_select) {
+      const int64_t g = env_i64("PINOT_AMD_SEL_GROUP", 4);
+      base.sel_group = g >= 4 ? 4 : g >= 2 ? 2 : 1;
+    }
     if (base.select && base.lds) {
       // gather blocks walk the selection vector grid-strided (padding included, matches unevenly spread
       // over its quads): one block may add every match of the batch to its LDS table, so the narrow
@@ -2885,7 +2891,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       ds.tile_begin = tiles;
       ds.key_seg = r->admit ? si : key_seg[si];
       ds.pad = r->admit ? 1 : 0;  // sequential admission over whole segments: each one walked to its end
-      tiles += (segs[si]->num_docs + kTileDocs - 1) / kTileDocs;
+      // (a tile-level select with G tiles per step: the segment's range padded to a multiple of G; the
+      // padding tiles match nothing and read only their columns' staging padding)
+      const int64_t G = base.select ? base.sel_group : 1;
+      tiles += ((segs[si]->num_docs + kTileDocs - 1) / kTileDocs + G - 1) / G * G;
       L.docs += segs[si]->num_docs;
       ls.push_back(ds);
       lbits.push_back(bitset_ptrs[si]);
@@ -3013,6 +3022,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         bpr += js.enc == ENC_FIXED_BIT ? (js.bits > 0 ? js.bits : 16) / 8.0 : js.enc == ENC_RAW ? value_size(js.type) : 0.0;
       }
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
+      // a select step of G tiles loads G tiles per register set: the same bytes in flight with 1/G the sets
+      if (jp.select && !jp.word_select && jp.sel_group > 1) jp.depth = std::max(1, (jp.depth + jp.sel_group - 1) / jp.sel_group);
       if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
       if (env_is("PINOT_AMD_LANE_TABLES", "0")) {
         for (auto& js : jp.slots) js.dict_regs = 0;
@@ -3215,8 +3226,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (value_slot[sl] && k == 0) L.value_bpr += bpr;
         }
       // Vector chunk a wave reserves at a time: about twice the matches a wave expects (plan-time
-      // counts), a power of two in [512, 4096] for the tile-level select (a run of up to 256 entries
-      // must fit a chunk) or [64, 4096] for the word-level one (runs split across chunks): few
+      // counts), a power of two in [512 G, max(4096, 512 G)] for the tile-level select of G tiles per step
+      // (a run of up to 256 G entries must fit a chunk) or [64, 4096] for the word-level one (runs split across chunks): few
       // reservations on the shared counter, little padding for the gather to read when matches are rare.
       int64_t m = 0, mt = 0;
       for (int si : L.segs) {  // + padding: one run per 256-doc wave tile, or per lane's 256 docs
@@ -3224,12 +3235,14 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         m += seg_matched[si] + 3 * std::min<int64_t>(seg_matched[si], (segs[si]->num_docs + 255) / 256 + 1);
       }
       const int64_t waves = (int64_t)cus * nb * 4;
-      int64_t chunk = jp.word_select ? 64 : 512;
-      while (chunk < 4096 && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
+      // (a tile-level step appends up to 256 x sel_group entries, which must fit one chunk)
+      const int64_t run_max = 256 * (int64_t)std::max(jp.sel_group, 1);
+      int64_t chunk = jp.word_select ? 64 : 2 * run_max;
+      while (chunk < std::max<int64_t>(4096, 2 * run_max) && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
       L.q.sel_chunk = (int32_t)chunk;
-      // a tile-level chunk holds >= chunk - 255 entries before the wave takes another; a word-level chunk
-      // is filled; every wave may leave its last chunk partly unused
-      const int64_t per_chunk = jp.word_select ? chunk : chunk - 255;
+      // a tile-level chunk holds >= chunk - run_max + 1 entries before the wave takes another; a word-level
+      // chunk is filled; every wave may leave its last chunk partly unused
+      const int64_t per_chunk = jp.word_select ? chunk : chunk - run_max + 1;
       const int64_t chunks = (m + per_chunk - 1) / per_chunk + waves + 1;
       max_sel = std::max<int64_t>(max_sel, chunks * chunk + 64);
     } else {

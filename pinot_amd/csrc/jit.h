@@ -139,6 +139,8 @@ struct JitPlan {
   // evaluates the CNF on 64-doc words
   bool word_select = false;
   int wsel_words = 4;  // word-level select: 64-doc words per lane and step (4 or 8; 16 words are one tile)
+  int sel_group = 1;   // tile-level select: 1024-doc tiles per loop step (1, 2 or 4; each segment's tile
+                       // range in the launch padded to a multiple of it)
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);
