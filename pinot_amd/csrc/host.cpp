@@ -1732,7 +1732,8 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
                                    L.fused_leaves, L.fused_clauses, L.q.sel_entries, L.q.sel_count, L.q.sel_cap,
                                    matched, L.fused_clause ? 1 : 0, st));
     else
-      HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, (unsigned)L.shmem_sets, st, args, nullptr));
+      // (select kernels hold their tables in static LDS)
+      HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
     if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
       unsigned long long ctr[2];
       HIP_OK(hipMemcpyAsync(ctr, L.q.sel_count, 16, hipMemcpyDeviceToHost, st));
@@ -3207,7 +3208,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.scan_nsub = 1;
       L.gather_threads = jp.lds ? kBlock * jp.scan_nsub : kBlock;
       int nb = 0, ng = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, L.shmem_sets) != hipSuccess || nb < 1) nb = 1;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
           ng < 1)
         ng = 1;
@@ -3219,6 +3220,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (const char* e = getenv("PINOT_AMD_SELECT_PER_CU")) nb = std::max(1, std::min(nb, atoi(e)));
       per_cu = nb;
       L.gather_grid = cus * ng;
+      if (const char* e = getenv("PINOT_AMD_GATHER_BLOCKS")) L.gather_grid = std::max(1, std::min(L.gather_grid, atoi(e)));
       for (size_t k = 0; k < L.segs.size(); ++k)
         for (int sl = 0; sl < nslots; ++sl) {
           const double bpr = slot_bpr(ls[k].cols[sl]);
