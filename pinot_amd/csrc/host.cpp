@@ -3227,24 +3227,21 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
           if (leaf_slot[sl]) L.filter_bytes += bpr * (double)ls[k].num_docs;
           if (value_slot[sl] && k == 0) L.value_bpr += bpr;
         }
-      // Vector chunk a wave reserves at a time: about twice the matches a wave expects (plan-time
-      // counts), a power of two in [512 G, max(4096, 512 G)] for the tile-level select of G tiles per step
-      // (a run of up to 256 G entries must fit a chunk) or [64, 4096] for the word-level one (runs split across chunks): few
-      // reservations on the shared counter, little padding for the gather to read when matches are rare.
+      // Vector chunk a wave reserves at a time (plan-time counts): a power of two in [256, 4096] for the
+      // tile-level select, [64, 4096] for the word-level one; runs split across chunks in both.
       int64_t m = 0, mt = 0;
       for (int si : L.segs) {  // + padding: one run per 256-doc wave tile, or per lane's 256 docs
         mt += seg_matched[si];
         m += seg_matched[si] + 3 * std::min<int64_t>(seg_matched[si], (segs[si]->num_docs + 255) / 256 + 1);
       }
       const int64_t waves = (int64_t)cus * nb * 4;
-      // (a tile-level step appends up to 256 x sel_group entries, which must fit one chunk)
-      const int64_t run_max = 256 * (int64_t)std::max(jp.sel_group, 1);
-      int64_t chunk = jp.word_select ? 64 : 2 * run_max;
-      while (chunk < std::max<int64_t>(4096, 2 * run_max) && chunk < 2 * mt / std::max<int64_t>(waves, 1)) chunk *= 2;
+      // (runs continue over chunk ends, so a chunk is filled: the only padding is each wave's last chunk's
+      // tail, written by the select and read by the gather -- a quarter of the matches a wave expects
+      // keeps it small without many reservations)
+      int64_t chunk = jp.word_select ? 64 : 256;
+      while (chunk < 4096 && chunk < mt / std::max<int64_t>(4 * waves, 1)) chunk *= 2;
       L.q.sel_chunk = (int32_t)chunk;
-      // a tile-level chunk holds >= chunk - run_max + 1 entries before the wave takes another; a word-level
-      // chunk is filled; every wave may leave its last chunk partly unused
-      const int64_t per_chunk = jp.word_select ? chunk : chunk - run_max + 1;
+      const int64_t per_chunk = chunk;
       const int64_t chunks = (m + per_chunk - 1) / per_chunk + waves + 1;
       max_sel = std::max<int64_t>(max_sel, chunks * chunk + 64);
     } else {

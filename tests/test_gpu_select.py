@@ -79,6 +79,28 @@ def test_forced_select_vs_oracle(engine, data, monkeypatch, qi, plan):
     assert res.algorithmic_bytes() > 0
 
 
+@pytest.mark.parametrize("group", ["1", "2"])
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_select_tile_groups_vs_oracle(engine, data, monkeypatch, qi, group):
+    """The select pass walks G tiles of one segment per loop step (default 4) over tile ranges padded to
+    multiples of G; 1 and 2 here, on the same ragged segments (1 .. 131072 docs: padding tiles in most
+    of them), must give the oracle's result too."""
+    monkeypatch.setenv("PINOT_AMD_SELECT", "always")
+    monkeypatch.setenv("PINOT_AMD_PARTITIONED", "0")
+    monkeypatch.setenv("PINOT_AMD_SEL_GROUP", group)
+    bufs, segs = data
+    q = QUERIES[qi]
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert "select" in res.kernel_info(), res.kernel_info()
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    from pinot_amd.query import parse_sql
+    qc = parse_sql(q)
+    fs = {i for i, a in enumerate(qc.aggregations) if a.func in ("SUM", "AVG") and
+          (a.column == "r_double" or (a.expr is not None and a.expr[0] != "COL"))}
+    assert_same_groups(res.groups(), og, fs)
+
+
 def test_cost_model_picks_select_for_selective_wide_rows(engine, monkeypatch):
     """0.3 % of docs pass a filter on a 6-bit column while the query aggregates three wide raw columns:
     the planner takes the selection-vector plan on its own; at 50 % it keeps the fused scan."""
