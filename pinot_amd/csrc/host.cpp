@@ -3238,8 +3238,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // (runs continue over chunk ends, so a chunk is filled: the only padding is each wave's last chunk's
       // tail, written by the select and read by the gather -- a quarter of the matches a wave expects
       // keeps it small without many reservations)
+      // (word level: about twice the matches a wave expects, its reservations measured as its bound)
       int64_t chunk = jp.word_select ? 64 : 256;
-      while (chunk < 4096 && chunk < mt / std::max<int64_t>(4 * waves, 1)) chunk *= 2;
+      const int64_t want = jp.word_select ? 2 * mt / std::max<int64_t>(waves, 1) : mt / std::max<int64_t>(4 * waves, 1);
+      while (chunk < 4096 && chunk < want) chunk *= 2;
       L.q.sel_chunk = (int32_t)chunk;
       const int64_t per_chunk = chunk;
       const int64_t chunks = (m + per_chunk - 1) / per_chunk + waves + 1;
