@@ -31,6 +31,7 @@
 
 namespace pamd {
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st);
+hipError_t launch_sext_hi(uint64_t* d_acc, int64_t n, const int32_t* arrs, int32_t narr, hipStream_t st);
 hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long long* out, hipStream_t st);
 hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc, int fd_acc,
                        int32_t nsegs, int64_t limit, const int64_t* bucket_base, uint32_t* hist,
@@ -1279,6 +1280,10 @@ struct pinot_amd_result {
   std::string plan_timing;
   // result compaction cache (valid until the next execution)
   bool compacted = false;
+  // HBM-table array indices of the whole-query-narrow sums' low words (JitAcc::hbm_narrow): their high
+  // words are set from the low words' signs at the plan's end
+  DevBuf d_sext;
+  int32_t n_sext = 0;
   int64_t ngroups = 0;
   std::vector<uint64_t> ckeys, cacc;  // per group: key words (hash) or dense key; all accumulator words
   ~pinot_amd_result() {
@@ -1983,6 +1988,9 @@ static int run_plan(pinot_amd_result* r) {
     for (size_t li = 0; li < nl; ++li)
       if (int rc = launch_one(r, r->launches[li], li, (uint64_t*)r->acc.p, H)) return rc;
   }
+  if (r->n_sext > 0)
+    HIP_OK(launch_sext_hi((uint64_t*)r->acc.p, r->kind == PLAN_HASH ? r->fcap : r->q.num_keys, (const int32_t*)r->d_sext.p,
+                          r->n_sext, st));
   HIP_OK(hipEventRecord(r->ev1, st));
   return 0;
 }
@@ -2876,6 +2884,45 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.batch = b;
       }
     }
+  }
+  // Whole-query-narrow integer sums (JitAcc::hbm_narrow): when a SUM's value range times all the query's
+  // docs fits int64, its adds into the HBM table need no carry, so they are one non-returning 64-bit atomic
+  // on the low word (the 128-bit add waits for the old value to carry into the high word) and the plan's
+  // end sets the high words from the low words' signs. Not for trimmed hash plans: their per-segment
+  // tables merge into the final table before the plan's end.
+  {
+    std::vector<int32_t> arrs;
+    if (!r->trim && q.nacc > 0 && !env_is("PINOT_AMD_HBM_NARROW", "0")) {
+      auto maxabs = [&](int sl) -> __int128 {
+        __int128 m = 0;
+        for (auto* s : segs) {
+          const Column& c = *s->cols.at(slot_cols[sl]);
+          if (!c.has_range) return -1;
+          const __int128 a = c.vmax < 0 ? -(__int128)c.vmax : (__int128)c.vmax;
+          const __int128 b = c.vmin < 0 ? -(__int128)c.vmin : (__int128)c.vmin;
+          m = std::max(m, std::max(a, b));
+        }
+        return m;
+      };
+      for (size_t ai = 0; ai < base.accs.size(); ++ai) {
+        JitAcc& a = base.accs[ai];
+        a.hbm_narrow = 0;
+        if (a.op != ACC_SUM_I128) continue;
+        __int128 m = maxabs(a.slot);
+        if (m >= 0 && a.expr != EXPR_COL) {
+          const __int128 m2 = maxabs(a.slot2);
+          m = m2 < 0 ? -1 : a.expr == EXPR_MUL ? m * m2 : m + m2;
+        }
+        if (m >= 0 && m * (__int128)std::max<int64_t>(all_docs, 1) <= (__int128)INT64_MAX) {
+          a.hbm_narrow = 1;
+          arrs.push_back((int32_t)ai + 1);  // HBM array of its low word (array 0 is COUNT)
+        }
+      }
+    }
+    r->n_sext = (int32_t)arrs.size();
+    r->d_sext.reset();
+    if (!arrs.empty())
+      if (int rc = r->d_sext.alloc_copy(arrs.data(), arrs.size() * 4, 0)) return rc;
   }
   const size_t nl = r->launches.size();
   if (int rc = r->matched.alloc((3 * nl + 2) * sizeof(unsigned long long))) return rc;

@@ -63,6 +63,11 @@ struct JitAcc {
   // int64 (ds_add_u64, no returned value to wait for) and the flush sign-extends it into the
   // 128-bit HBM sum
   int narrow = 0;
+  // ACC_SUM_I128 whose whole-query sum provably fits int64 (value range x all docs of the query): the
+  // per-doc (and per-block flush) adds into the HBM table are one non-returning 64-bit atomic on the low
+  // word -- no returned value to wait for the carry -- and the plan sets each high word to the low word's
+  // sign at its end (sext_hi_kernel), the 128-bit sum the readers expect
+  int hbm_narrow = 0;
   JitVal val() const { return JitVal{expr, slot, slot2}; }
 };
 struct JitPlan {

@@ -96,6 +96,18 @@ __global__ void init_acc_kernel(uint64_t* acc, int64_t num_keys, DevQuery q) {
     acc[i] = acc_identity(q.acc_op[i / num_keys]);
 }
 
+// The plan's end for whole-query-narrow 128-bit sums (JitAcc::hbm_narrow): their low words were added mod
+// 2^64 with non-returning atomics (no carries), and the true sums fit int64, so each high word is the low
+// word's sign. acc[lo * n + i] / acc[(lo + 1) * n + i] for every array index lo in arrs.
+__global__ void sext_hi_kernel(uint64_t* acc, int64_t n, const int32_t* arrs, int32_t narr) {
+  for (int32_t a = 0; a < narr; ++a) {
+    const uint64_t* lo = acc + (int64_t)arrs[a] * n;
+    uint64_t* hi = acc + (int64_t)(arrs[a] + 1) * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+      hi[i] = (int64_t)lo[i] < 0 ? ~0ull : 0ull;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Hash-table GROUP BY passes (DevHash layout; the scan itself is the JIT kernel)
 // ------------------------------------------------------------------------------------------------
@@ -1310,6 +1322,13 @@ hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long lo
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(raw_int_minmax_kernel, dim3(g), dim3(kBlock), 0, st, be, type, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sext_hi(uint64_t* d_acc, int64_t n, const int32_t* arrs, int32_t narr, hipStream_t st) {
+  unsigned g = grid_for(n, kBlock);
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(sext_hi_kernel, dim3(g), dim3(kBlock), 0, st, d_acc, n, arrs, narr);
   return hipGetLastError();
 }
 
