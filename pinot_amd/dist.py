@@ -38,6 +38,11 @@ def init_distributed():
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # rehearsal of the N-rank path on a one-GPU box: every rank on device 0, collectives over gloo
+        # (RCCL needs a device per rank)
+        backend = os.environ.get("PINOT_AMD_DIST_BACKEND", backend)
+        if os.environ.get("PINOT_AMD_DIST_ONE_DEVICE") == "1":
+            local = 0
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
