@@ -2797,6 +2797,14 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const int64_t g = env_i64("PINOT_AMD_SEL_GROUP", 4);
       base.sel_group = g >= 4 ? 4 : g >= 2 ? 2 : 1;
     }
+  }
+  // a fused scan of a dense plan with tile groups too (PINOT_AMD_SCAN_GROUP, default 4: configs[1] 3.45 -> 3.38 ms,
+  // SSB Q3.1 0.896 -> 0.858 ms)
+  if (!base.select && r->kind == PLAN_DENSE && !base.partitioned && !r->admit && !filter_only) {
+    const int64_t g = env_i64("PINOT_AMD_SCAN_GROUP", 4);
+    base.sel_group = g >= 4 ? 4 : g >= 2 ? 2 : 1;
+  }
+  {
     if (base.select && base.lds) {
       // gather blocks walk the selection vector grid-strided (padding included, matches unevenly spread
       // over its quads): one block may add every match of the batch to its LDS table, so the narrow
@@ -2941,7 +2949,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       ds.pad = r->admit ? 1 : 0;  // sequential admission over whole segments: each one walked to its end
       // (a tile-level select with G tiles per step: the segment's range padded to a multiple of G; the
       // padding tiles match nothing and read only their columns' staging padding)
-      const int64_t G = base.select ? base.sel_group : 1;
+      const int64_t G = base.sel_group;
       tiles += ((segs[si]->num_docs + kTileDocs - 1) / kTileDocs + G - 1) / G * G;
       L.docs += segs[si]->num_docs;
       ls.push_back(ds);
@@ -3071,7 +3079,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
       // a select step of G tiles loads G tiles per register set: the same bytes in flight with 1/G the sets
-      if (jp.select && !jp.word_select && jp.sel_group > 1) jp.depth = std::max(1, (jp.depth + jp.sel_group - 1) / jp.sel_group);
+      if (jp.sel_group > 1) jp.depth = std::max(1, (jp.depth + jp.sel_group - 1) / jp.sel_group);
       if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
       if (env_is("PINOT_AMD_LANE_TABLES", "0")) {
         for (auto& js : jp.slots) js.dict_regs = 0;
