@@ -800,7 +800,9 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
   }
   if (rc) return rc;
   if (c->enc != ENC_RAW) {
-    if (!spec->h_dictionary) return fail(PINOT_AMD_EINVAL, "column %s: dictionary required", spec->name);
+    // (a column without documents may have an empty dictionary)
+    if (!spec->h_dictionary && !(c->card == 0 && spec->dictionary_size == 0))
+      return fail(PINOT_AMD_EINVAL, "column %s: dictionary required", spec->name);
     rc = decode_dictionary(*c, (const uint8_t*)spec->h_dictionary, spec->dictionary_size);
     if (rc) return rc;
     if (!c->dict_i.empty()) {  // INT / LONG dictionaries are sorted

@@ -480,6 +480,8 @@ def inverted_index_bytes_fast(dict_ids: np.ndarray, cardinality: int) -> Optiona
 
 def inverted_index_bytes(dict_ids: np.ndarray, cardinality: int) -> bytes:
     """BitmapInvertedIndexWriter layout: (cardinality+1) BE absolute offsets, then bitmaps."""
+    if cardinality == 0:  # an empty column: the header's one offset (the end) and no bitmaps
+        return (4).to_bytes(4, "big")
     fast = inverted_index_bytes_fast(dict_ids, cardinality)
     if fast is not None:
         return fast
