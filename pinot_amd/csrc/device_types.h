@@ -147,7 +147,8 @@ struct ChunkJob {
 
 // Hash-table group-by (key spaces a dense table cannot hold, and numGroupsLimit trimming): open
 // addressing with linear probing over `cap` slots. A key is `nwords` 64-bit words (the group columns'
-// merged ids packed <= 63 bits per word, so no word is ever ~0; trimming plans add the batch segment
+// merged ids packed <= 63 bits per word, or 64 when one of the word's fields can never be all ones, so no
+// word is ever ~0 (host.cpp pack_key_words); trimming plans add the batch segment
 // index as the last word), stored word-major at keys[w * cap + slot]; EMPTY words are ~0. A slot is
 // claimed word by word with compare-and-swap: whoever sets word w decides it, a thread finding a
 // different word moves on to the next slot, so a slot's key is complete once every thread that

@@ -1997,6 +1997,31 @@ static int run_plan(pinot_amd_result* r) {
   return 0;
 }
 
+// Hash-plan key words: the group columns' merged ids packed low to high. EMPTY (~0) must stay impossible
+// for every word: a word takes a field while it stays within 63 bits, or fills all 64 bits when one of its
+// fields can never be all ones (a key space smaller than 2^bits: its largest id leaves a zero bit) -- the
+// wide-key bench's 5 ids (15 + 15 + 15 + 10 + 9 bits) then fit one word instead of two.
+static int bits_for(int64_t card);
+static void pack_key_words(const std::vector<int64_t>& sizes, std::vector<int>* word, std::vector<int>* shift) {
+  int w = 0, sh = 0;
+  bool safe = false;  // the current word has a field that is never all ones
+  word->clear();
+  shift->clear();
+  for (int64_t size : sizes) {
+    const int b = bits_for(size);
+    const bool never_ones = size < ((int64_t)1 << b);
+    if (sh + b > 64 || (sh + b == 64 && !(safe || never_ones))) {
+      ++w;
+      sh = 0;
+      safe = false;
+    }
+    word->push_back(w);
+    shift->push_back(sh);
+    sh += b;
+    safe |= never_ones;
+  }
+}
+
 static int64_t next_pow2(int64_t x) {
   int64_t c = 1;
   while (c < x) c <<= 1;
@@ -2401,16 +2426,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const int64_t table_budget = env_i64("PINOT_AMD_HASH_TABLE_BYTES", (int64_t)4 << 30);  // per trim scan table
   std::vector<int> seg_batch(n, 0);
   if (r->kind == PLAN_HASH) {
-    int w = 0, sh = 0;
-    for (auto& m : r->keys) {
-      const int b = bits_for((int64_t)std::max<size_t>(m.size(), 1));
-      if (sh + b > 63) { ++w; sh = 0; }
-      r->pack_word.push_back(w);
-      r->pack_shift.push_back(sh);
-      r->pack_bits.push_back(b);
-      sh += b;
-    }
-    r->nw = w + 1;
+    std::vector<int64_t> sizes;
+    for (auto& m : r->keys) sizes.push_back((int64_t)std::max<size_t>(m.size(), 1));
+    pack_key_words(sizes, &r->pack_word, &r->pack_shift);
+    r->pack_bits.clear();
+    for (int64_t sz : sizes) r->pack_bits.push_back(bits_for(sz));
+    r->nw = r->pack_word.empty() ? 1 : r->pack_word.back() + 1;
     if (r->nw + (r->trim ? 1 : 0) > kMaxKeyWords)
       return fail(PINOT_AMD_EUNSUPPORTED, "group key of %d words exceeds %d", r->nw, kMaxKeyWords);
     const double keyspace = dense_keys;
@@ -3996,18 +4017,17 @@ static int key_pack(const pinot_amd_result* r, DevKeyPack* kp) {
   memset(kp, 0, sizeof(*kp));
   kp->ncols = r->num_group_by;
   if (kp->ncols > kMaxGroupCols) return fail(PINOT_AMD_EUNSUPPORTED, "export: %d group columns", kp->ncols);
-  int w = 0, sh = 0;
+  std::vector<int64_t> sizes;
+  for (int j = 0; j < kp->ncols; ++j) sizes.push_back((int64_t)std::max<size_t>(r->keys[j].size(), 1));
+  std::vector<int> word, shift;
+  pack_key_words(sizes, &word, &shift);  // the hash plan's packing
   for (int j = 0; j < kp->ncols; ++j) {
-    const int64_t size = (int64_t)std::max<size_t>(r->keys[j].size(), 1);
-    const int b = bits_for(size);
-    if (sh + b > 63) { ++w; sh = 0; }
-    kp->word[j] = w;
-    kp->shift[j] = sh;
-    kp->size[j] = size;
+    kp->word[j] = word[j];
+    kp->shift[j] = shift[j];
+    kp->size[j] = sizes[j];
     kp->stride[j] = j < (int)r->key_stride.size() ? std::max<int64_t>(r->key_stride[j], 1) : 1;
-    sh += b;
   }
-  kp->nw = w + 1;
+  kp->nw = word.empty() ? 1 : word.back() + 1;
   if (kp->nw > kMaxKeyWords) return fail(PINOT_AMD_EUNSUPPORTED, "group key of %d words exceeds %d", kp->nw, kMaxKeyWords);
   return 0;
 }
