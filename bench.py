@@ -285,6 +285,7 @@ def main():
         # device time of each step's plan: HIP events recorded on the plan's own stream around the execution
         # (no host sync inside the timed loop; read after it)
         ev_pairs = []
+        merge_ev = []  # (N > 1) HIP events around each timed step's merge on the same stream
 
         def step(timed=False):
             nonlocal scratch
@@ -297,6 +298,10 @@ def main():
                 ev_pairs.append((e0, e1))
             if world > 1:
                 scratch = pdist.merge_result(res, scratch, stream=stream)
+                if timed:
+                    e2 = torch.cuda.Event(enable_timing=True)
+                    e2.record(stream)
+                    merge_ev.append((e1, e2))
 
         for _ in range(args.warmup):
             step()
@@ -319,6 +324,30 @@ def main():
 
         total_rows = rows_per_rank * world * args.steps
         value = total_rows / elapsed
+        merge = None
+        if world > 1:
+            # the cross-rank merge alone (the broker reduce's share of a step): HIP events around it inside the
+            # timed steps, and, untimed afterwards, a few merges bracketed by device synchronisation (wall
+            # clock, max over ranks) -- so a poor scaling curve says whether the scan or the merge is to blame
+            ms_ev = sum(a.elapsed_time(b) for a, b in merge_ev) / max(len(merge_ev), 1)
+            walls = []
+            for _ in range(3):
+                res.execute_again(stream)  # a fresh, unmerged table each time (a merge is not idempotent)
+                torch.cuda.synchronize()
+                dist.barrier()
+                t_m = time.perf_counter()
+                scratch = pdist.merge_result(res, scratch, stream=stream)
+                torch.cuda.synchronize()
+                walls.append(time.perf_counter() - t_m)
+            w = torch.tensor([sum(walls) / len(walls)], dtype=torch.float64,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(w, op=dist.ReduceOp.MAX)
+            st = (scratch or {}).get("stats", {}) if isinstance(scratch, dict) else {}
+            merge = {"path": st.get("path"), "bytes_per_rank": st.get("bytes"), "ms_events": ms_ev,
+                     "ms_wall_synchronized": float(w.item()) * 1e3, "backend": dist.get_backend(),
+                     "source": "ms_events: HIP events on the step's stream around pdist.merge_result in the timed "
+                               "steps; ms_wall_synchronized: 3 untimed merges between device synchronisations, "
+                               "mean per rank, max over ranks"}
         kernel_ms = [a.elapsed_time(b) for a, b in ev_pairs]
         lib_kernel_ms = res.last_kernel_ms()  # the library's own events around the last execution (cross-check)
         avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -427,6 +456,8 @@ def main():
                 },
                 "cpu_baseline": cpu,
             }
+            if merge is not None:
+                out["merge"] = merge
             print(json.dumps(out), flush=True)
             outs.append(out)
         res.destroy()

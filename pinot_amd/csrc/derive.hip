@@ -147,4 +147,62 @@ hipError_t derive_dictionary(const uint8_t* d_be, int type, int64_t n, void* d_s
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Compacted hash-table groups in ascending key order (the order a dense table's groups come in): a
+// hash plan's packed key words compare, as one (nwk x 64)-bit integer with word nwk - 1 most
+// significant, exactly as the group columns' merged ids from the last column to the first, so a stable
+// LSD radix sort over the words -- least significant word first, each pass sorting (word, row) pairs in
+// the order the previous passes left -- yields the permutation; the rows are then gathered.
+// ------------------------------------------------------------------------------------------------
+__global__ void key_word_kernel(const uint64_t* keys, int nwk, int w, const uint32_t* idx, int64_t n, uint64_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = keys[(idx ? (int64_t)idx[i] : i) * nwk + w];
+}
+__global__ void iota_kernel(uint32_t* idx, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    idx[i] = (uint32_t)i;
+}
+__global__ void gather_rows_kernel(const uint64_t* src, int width, const uint32_t* idx, int64_t n, uint64_t* dst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * width; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / width, c = i - r * width;
+    dst[i] = src[(int64_t)idx[r] * width + c];
+  }
+}
+
+size_t sort_rows_scratch(int64_t n) {
+  size_t sort_bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned int)n, 0, 64);
+  return (size_t)n * (8 + 8 + 4 + 4) + sort_bytes + 512;
+}
+
+// keys: n rows of nwk words (row-major), acc: n rows of nacc words; word_bits[w]: bits word w can use.
+// Rows written to keys_out / acc_out in ascending key order.
+hipError_t sort_rows_by_key(const uint64_t* keys, int nwk, const int* word_bits, const uint64_t* acc, int nacc, int64_t n,
+                            void* scratch, uint64_t* keys_out, uint64_t* acc_out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
+  uint64_t* kw = reinterpret_cast<uint64_t*>(p);
+  uint64_t* kw2 = kw + n;
+  uint32_t* idx = reinterpret_cast<uint32_t*>(kw2 + n);
+  uint32_t* idx2 = idx + n;
+  void* tmp = reinterpret_cast<void*>(((uintptr_t)(idx2 + n) + 255) & ~(uintptr_t)255);
+  size_t sort_bytes = 0;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, sort_bytes, kw, kw2, idx, idx2, (unsigned int)n, 0, 64, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(iota_kernel, dim3(grid_of(n)), dim3(256), 0, st, idx, n);
+  for (int w = 0; w < nwk; ++w) {
+    hipLaunchKernelGGL(key_word_kernel, dim3(grid_of(n)), dim3(256), 0, st, keys, nwk, w, (const uint32_t*)idx, n, kw);
+    const unsigned end_bit = (unsigned)(word_bits[w] < 1 ? 1 : word_bits[w] > 64 ? 64 : word_bits[w]);
+    e = rocprim::radix_sort_pairs(tmp, sort_bytes, kw, kw2, idx, idx2, (unsigned int)n, 0u, end_bit, st);
+    if (e != hipSuccess) return e;
+    uint32_t* t = idx;  // the sorted permutation becomes the next pass's input order
+    idx = idx2;
+    idx2 = t;
+  }
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_of(n * nwk)), dim3(256), 0, st, keys, nwk, (const uint32_t*)idx, n, keys_out);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_of(n * nacc)), dim3(256), 0, st, acc, nacc, (const uint32_t*)idx, n, acc_out);
+  return hipGetLastError();
+}
+
 }  // namespace pamd

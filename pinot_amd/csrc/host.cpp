@@ -16,6 +16,7 @@
 #include <climits>
 #include <limits>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -58,6 +59,9 @@ hipError_t launch_read_dict_ids(const uint8_t* packed, int bits, int64_t start, 
                                 hipStream_t st);
 hipError_t launch_pack_dict_ids(const int32_t* values, int64_t n, int bits, uint8_t* packed, hipStream_t st);
 size_t derive_dictionary_scratch(int64_t n);
+size_t sort_rows_scratch(int64_t n);
+hipError_t sort_rows_by_key(const uint64_t* keys, int nwk, const int* word_bits, const uint64_t* acc, int nacc, int64_t n,
+                            void* scratch, uint64_t* keys_out, uint64_t* acc_out, hipStream_t st);
 hipError_t derive_dictionary(const uint8_t* d_be, int type, int64_t n, void* d_scratch, int32_t* d_ids,
                              uint8_t* d_dict_be, int64_t* h_card, hipStream_t st);
 hipError_t launch_read_raw(const uint8_t* raw, int type, int64_t start, int64_t len, uint8_t* out, hipStream_t st);
@@ -678,7 +682,10 @@ int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segme
   return 0;
 }
 
+static void drop_segment_caches(uint64_t uid);
+
 int pinot_amd_segment_destroy(pinot_amd_segment* seg) {
+  if (seg) drop_segment_caches(seg->uid);  // merged key spaces and remaps over it (host.cpp key caches)
   delete seg;
   return 0;
 }
@@ -974,14 +981,25 @@ struct MergedKeyColumn {
   std::vector<int64_t> vi;
   std::vector<double> vd;
   std::vector<std::string> vs;
+  uint64_t id = 0;  // process-unique identity of this key space (keys the per-segment remap cache)
   size_t size() const { return type == T_STRING ? vs.size() : is_float(type) ? vd.size() : vi.size(); }
+  size_t host_bytes() const {
+    size_t b = sizeof(*this) + vi.size() * 8 + vd.size() * 8;
+    for (const std::string& s : vs) b += sizeof(std::string) + s.size();
+    return b;
+  }
 };
+static uint64_t next_key_space_id() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1);
+}
 
 struct pinot_amd_query {
   std::vector<PredSpec> preds;
   std::vector<std::string> group_by;
-  // group-by column -> key space installed by the caller (the union of every server's dictionaries)
-  std::map<std::string, MergedKeyColumn> key_space;
+  // group-by column -> key space installed by the caller (the union of every server's dictionaries); shared,
+  // immutable once installed (every plan of the query reads the same one, never a copy)
+  std::map<std::string, std::shared_ptr<const MergedKeyColumn>> key_space;
   std::vector<AggSpec> aggs;
   int64_t num_groups_limit = 100000;
   // server-level IndexedTable of the combine (GroupByUtils.createIndexedTableForCombineOperator):
@@ -1085,6 +1103,7 @@ int pinot_amd_query_set_group_key_values(pinot_amd_query* q, const char* column,
     return fail(PINOT_AMD_EINVAL, "set_group_key_values: bad arguments");
   MergedKeyColumn m;
   m.type = stored_type;
+  m.id = next_key_space_id();
   for (int64_t i = 0; i < n; ++i) {
     if (stored_type == T_STRING) {
       if (!h_values_s || !h_values_s[i]) return fail(PINOT_AMD_EINVAL, "set_group_key_values: null string");
@@ -1110,7 +1129,7 @@ int pinot_amd_query_set_group_key_values(pinot_amd_query* q, const char* column,
     std::sort(m.vi.begin(), m.vi.end());
     m.vi.erase(std::unique(m.vi.begin(), m.vi.end()), m.vi.end());
   }
-  q->key_space[column] = std::move(m);
+  q->key_space[column] = std::make_shared<const MergedKeyColumn>(std::move(m));
   return 0;
 }
 
@@ -1225,7 +1244,8 @@ struct pinot_amd_result {
   // counters: 3 per launch ([0] count pass / scan matches, [1] sampled matches, [2] direct-atomic
   // scan matches), then numGroupsLimitReached, then hash overflow
   DevBuf matched;
-  std::vector<MergedKeyColumn> keys;  // merged dictionaries of the group-by columns
+  std::vector<std::shared_ptr<const MergedKeyColumn>> keys;  // merged dictionaries of the group-by columns
+  std::vector<std::shared_ptr<DevBuf>> shared;  // device buffers shared with the planner's caches (remaps)
   std::vector<int64_t> key_stride;    // dense: mixed-radix strides
   std::vector<int32_t> agg_acc;        // aggregation -> accumulator index (AVG: sum acc; MINMAXRANGE: min acc)
   std::vector<int32_t> agg_acc2;       // MINMAXRANGE: max acc
@@ -1244,6 +1264,13 @@ struct pinot_amd_result {
   std::vector<int> pack_word, pack_shift, pack_bits;
   DevBuf fkeys;                        // final table keys (nw x fcap)
   int64_t fcap = 0;
+  // untrimmed hash plans: the table grows 4x (up to fcap_ceiling: 2 x the plan's group bound, the slot and
+  // byte limits) while docs find no slot. The capacity an execution settled on is remembered per (query
+  // shape, segment set) (cap_key); a plan that starts from it runs without the host synchronisation that
+  // reads the overflow counter (ovf_pending: check_overflow settles it when the groups are read)
+  int64_t fcap_ceiling = 0;
+  std::string cap_key;
+  bool cap_known = false, ovf_pending = false;
   bool trim = false;                   // numGroupsLimit trimming (scan tables keyed by (key, segment))
   int64_t limit = 100000;
   bool limit_possible = false;         // some segment may hold >= numGroupsLimit keys
@@ -1269,6 +1296,7 @@ struct pinot_amd_result {
   // group compaction scratch (presence bits, chunk counts, total, slot indices, gathered keys / accumulators),
   // kept across fetches and executions: a fetch allocates nothing on the device
   DevBuf c_bits, c_counts, c_total, c_idx, c_okeys, c_oacc;
+  DevBuf c_skeys, c_sacc, c_sscratch;  // hash groups sorted by key on the device (sort_rows_by_key)
   int64_t mcap = 0;
   int mnw = 0;
   // server-level IndexedTable (pinot_amd_query_set_result_limit / add_order_by), applied at compaction
@@ -1409,6 +1437,9 @@ static bool use_inverted_for(const Column& c, int64_t num_docs, const std::vecto
   const double scan_cost = decoded_anyway ? 0.0 : (double)num_docs * c.bits / 8.0;
   return inv_cost < scan_cost;
 }
+
+// docId-bitset slack behind an inverted-index leaf's words (make_leaf_for_segment): 64 tiles
+constexpr size_t kBitsetSlackBytes = 64 * kTileDocs / 8;
 
 static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_segment* seg, const PredSpec& p,
                                  const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
@@ -1559,8 +1590,11 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
         for (uint32_t k = c.inv_dir[d]; k < c.inv_dir[d + 1]; ++k)
           if (c.inv_keys[k] < nchunks) sel[fillp[c.inv_keys[k] / G]++] = (int32_t)k;
     }
+    // (+ slack: grouped scan / select steps read the word of every lane's doc0 in padding tiles and in the
+    // inactive steps past a block's range -- up to (D + 1) x G + 3 tiles beyond the segment -- whose masks are
+    // zero; the words are allocated so those reads stay inside the buffer)
     auto bs = std::make_unique<DevBuf>();
-    int rc = bs->alloc(bs_bytes);
+    int rc = bs->alloc(bs_bytes + kBitsetSlackBytes);
     if (rc) return rc;
     auto sb = std::make_unique<DevBuf>();
     rc = sb->alloc_copy(sel.data(), sel.size() * 4, 64);
@@ -1658,26 +1692,80 @@ static int build_merged_keys_uncached(const std::vector<pinot_amd_segment*>& seg
 
 // Merged dictionaries of a group-by column over a segment set, cached per (column, segments): segments are
 // immutable, and every query grouping by the column over the same batch merges the same dictionaries (SSB
-// Q2.x: 60 dictionaries of 1000 brands, ~5 ms per query).
+// Q2.x: 60 dictionaries of 1000 brands, ~5 ms per query). Entries are shared (never copied into a plan),
+// least-recently-used entries go beyond a host-byte budget (PINOT_AMD_KEY_CACHE_BYTES, default 1 GiB), and
+// an entry goes with the first of its segments that is destroyed.
+// Per-segment remaps (dictId -> id in a merged key space) are cached the same way, keyed by (segment, column,
+// key-space id): the device array a plan reads, shared with every plan that uses it (SSB Q2.x planning spent
+// ~2 ms per query, the wide-key bench ~110 ms, in binary searches over the merged dictionaries).
+struct KeyCacheEntry {
+  std::shared_ptr<const MergedKeyColumn> keys;
+  std::vector<uint64_t> uids;
+  size_t bytes = 0;
+  uint64_t used = 0;
+};
+struct RemapCacheEntry {
+  std::shared_ptr<DevBuf> buf;  // nullptr: the identity (no remap needed)
+  uint64_t uid = 0, used = 0;
+};
 static std::mutex g_keys_mu;
-static std::map<std::string, std::shared_ptr<const MergedKeyColumn>> g_keys_cache;
+static std::map<std::string, KeyCacheEntry> g_keys_cache;
+static std::map<std::string, RemapCacheEntry> g_remap_cache;
+static size_t g_keys_bytes = 0;
+static uint64_t g_cache_clock = 0;
+
+static void drop_segment_caches(uint64_t uid) {
+  std::lock_guard<std::mutex> g(g_keys_mu);
+  for (auto it = g_keys_cache.begin(); it != g_keys_cache.end();) {
+    if (std::find(it->second.uids.begin(), it->second.uids.end(), uid) != it->second.uids.end()) {
+      g_keys_bytes -= it->second.bytes;
+      it = g_keys_cache.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  for (auto it = g_remap_cache.begin(); it != g_remap_cache.end();)
+    it = it->second.uid == uid ? g_remap_cache.erase(it) : std::next(it);
+}
 
 static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const std::string& col,
-                             MergedKeyColumn* out) {
+                             std::shared_ptr<const MergedKeyColumn>* out) {
   std::string key = col + "|";
   for (auto* sg : segs) key += std::to_string(sg->uid) + "." + std::to_string(sg->gen) + ",";
   {
     std::lock_guard<std::mutex> g(g_keys_mu);
     auto it = g_keys_cache.find(key);
     if (it != g_keys_cache.end()) {
-      *out = *it->second;
+      it->second.used = ++g_cache_clock;
+      *out = it->second.keys;
       return 0;
     }
   }
-  if (int rc = build_merged_keys_uncached(segs, col, out)) return rc;
+  MergedKeyColumn m;
+  if (int rc = build_merged_keys_uncached(segs, col, &m)) return rc;
+  m.id = next_key_space_id();
+  *out = std::make_shared<const MergedKeyColumn>(std::move(m));
+  KeyCacheEntry ent;
+  ent.keys = *out;
+  ent.bytes = (*out)->host_bytes() + key.size();
+  for (auto* sg : segs) ent.uids.push_back(sg->uid);
+  static const size_t budget = []() {
+    const char* v = getenv("PINOT_AMD_KEY_CACHE_BYTES");
+    return v ? (size_t)std::max(0ll, atoll(v)) : (size_t)1 << 30;
+  }();
   std::lock_guard<std::mutex> g(g_keys_mu);
-  if (g_keys_cache.size() >= 256) g_keys_cache.clear();  // bounded: a server's working set of batches
-  g_keys_cache[key] = std::make_shared<const MergedKeyColumn>(*out);
+  if (g_keys_cache.count(key)) return 0;  // another planner built it meanwhile
+  while (!g_keys_cache.empty() && g_keys_bytes + ent.bytes > budget) {  // least recently used first
+    auto lru = g_keys_cache.begin();
+    for (auto it = g_keys_cache.begin(); it != g_keys_cache.end(); ++it)
+      if (it->second.used < lru->second.used) lru = it;
+    g_keys_bytes -= lru->second.bytes;
+    g_keys_cache.erase(lru);
+  }
+  if (ent.bytes > budget) return 0;  // larger than the whole budget: not cached
+  ent.used = ++g_cache_clock;
+  g_keys_bytes += ent.bytes;
+  g_keys_cache[key] = std::move(ent);
   return 0;
 }
 
@@ -1719,6 +1807,43 @@ static int remap_for(const Column& c, const MergedKeyColumn& m, std::vector<int3
       pos = std::lower_bound(m.vi.begin(), m.vi.end(), c.dict_i[d]) - m.vi.begin();
     (*out)[d] = (int32_t)pos;
   }
+  return 0;
+}
+
+// the device remap of segment s's column c into key space m (cached, shared); *out = nullptr: the identity
+static int cached_remap(const pinot_amd_segment* s, const std::string& col, const Column& c, const MergedKeyColumn& m,
+                        std::shared_ptr<DevBuf>* out) {
+  const std::string key = std::to_string(s->uid) + "." + std::to_string(s->gen) + "|" + col + "|" + std::to_string(m.id);
+  if (m.id != 0) {
+    std::lock_guard<std::mutex> g(g_keys_mu);
+    auto it = g_remap_cache.find(key);
+    if (it != g_remap_cache.end()) {
+      it->second.used = ++g_cache_clock;
+      *out = it->second.buf;
+      return 0;
+    }
+  }
+  std::vector<int32_t> rm;
+  remap_for(c, m, &rm);
+  bool identity = (int64_t)rm.size() == (int64_t)m.size();
+  for (size_t d = 0; identity && d < rm.size(); ++d) identity = rm[d] == (int32_t)d;
+  out->reset();
+  if (!identity) {
+    auto buf = std::make_shared<DevBuf>();
+    if (int rc = buf->alloc_copy(rm.data(), rm.size() * 4, 64)) return rc;
+    *out = std::move(buf);
+  }
+  if (m.id == 0) return 0;
+  std::lock_guard<std::mutex> g(g_keys_mu);
+  if (g_remap_cache.size() >= 16384) {  // bounded: drop the least recently used quarter
+    std::vector<uint64_t> ages;
+    for (auto& kv : g_remap_cache) ages.push_back(kv.second.used);
+    std::nth_element(ages.begin(), ages.begin() + ages.size() / 4, ages.end());
+    const uint64_t cut = ages[ages.size() / 4];
+    for (auto it = g_remap_cache.begin(); it != g_remap_cache.end();)
+      it = it->second.used <= cut ? g_remap_cache.erase(it) : std::next(it);
+  }
+  g_remap_cache[key] = RemapCacheEntry{*out, s->uid, ++g_cache_clock};
   return 0;
 }
 
@@ -1908,8 +2033,44 @@ static int run_admission(pinot_amd_result* r, unsigned long long* limit_flag) {
   return 0;
 }
 
+// Hash-table capacities that held a query's groups, per (query shape, segment set) (pinot_amd_result::cap_key):
+// a re-issued query starts at the grown capacity instead of growing from PINOT_AMD_HASH_INIT_SLOTS again.
+static std::mutex g_cap_mu;
+static std::unordered_map<std::string, int64_t> g_cap_cache;
+
+static void remember_hash_capacity(pinot_amd_result* r) {
+  r->cap_known = true;
+  if (r->cap_key.empty()) return;
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  if (g_cap_cache.size() >= 4096) g_cap_cache.clear();
+  int64_t& c = g_cap_cache[r->cap_key];
+  c = std::max(c, r->fcap);
+}
+static int64_t known_hash_capacity(const std::string& key) {
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  auto it = g_cap_cache.find(key);
+  return it == g_cap_cache.end() ? 0 : it->second;
+}
+
+// grow an untrimmed hash plan's table 4x, at most to its ceiling (*grown false: already there)
+static int grow_hash(pinot_amd_result* r, bool* grown) {
+  *grown = false;
+  if (r->fcap >= r->fcap_ceiling) return 0;
+  const int64_t ncap = std::min(r->fcap * 4, r->fcap_ceiling);
+  r->fkeys.reset();
+  r->acc.reset();
+  if (int rc = r->fkeys.alloc((size_t)r->nw * (size_t)ncap * 8)) return rc;
+  if (int rc = r->acc.alloc((size_t)r->q.nacc * (size_t)ncap * 8)) return rc;
+  r->fcap = ncap;
+  r->compacted = false;
+  r->cap_known = false;
+  *grown = true;
+  return 0;
+}
+
 static int run_plan(pinot_amd_result* r) {
   r->merged = false;
+  r->ovf_pending = false;
   hipStream_t st = r->stream;
   r->compacted = false;
   HIP_OK(hipEventRecord(r->ev0, st));
@@ -1965,21 +2126,23 @@ static int run_plan(pinot_amd_result* r) {
     if (r->trim) break;
     // The table's capacity comes from a group-count bound (docs per segment, key space); real group counts
     // are usually far lower, so the plan starts small (PINOT_AMD_HASH_INIT_SLOTS) and, like the map-based
-    // holders that resize as groups arrive, grows 4x when some doc found no slot (then runs again).
+    // holders that resize as groups arrive, grows 4x when some doc found no slot (then runs again). A
+    // capacity an earlier execution of this query settled on needs no check here: no host synchronisation
+    // in the execution (check_overflow reads the counter with the groups and grows then if it must).
+    if (r->cap_known) {
+      r->ovf_pending = true;
+      break;
+    }
     unsigned long long ovf = 0;
     HIP_OK(hipMemcpyAsync(&ovf, overflow, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (ovf == 0) break;
-    const int64_t ncap = r->fcap * 4;
-    const double nbytes = (double)ncap * (double)(r->nw + r->q.nacc) * 8.0;
-    if (ncap > ((int64_t)1 << 31) || nbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
-      break;  // the overflow counter stays set: the result reports EOVERFLOW
-    r->fkeys.reset();
-    r->acc.reset();
-    if (int rc = r->fkeys.alloc((size_t)r->nw * (size_t)ncap * 8)) return rc;
-    if (int rc = r->acc.alloc((size_t)r->q.nacc * (size_t)ncap * 8)) return rc;
-    r->fcap = ncap;
-    r->compacted = false;
+    if (ovf == 0) {
+      remember_hash_capacity(r);
+      break;
+    }
+    bool grown = false;
+    if (int rc = grow_hash(r, &grown)) return rc;
+    if (!grown) break;  // at the ceiling: the overflow counter stays set, the result reports EOVERFLOW
     HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
    }
   } else {
@@ -2183,26 +2346,39 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   double dense_keys = 1;
   for (size_t j = 0; j < Q.group_by.size(); ++j) {
     const std::string& g = Q.group_by[j];
-    MergedKeyColumn m;
+    std::shared_ptr<const MergedKeyColumn> m;
     if (int rc = build_merged_keys(segs, g, &m)) return rc;
     auto ks = qq->key_space.find(qq->group_by[j]);  // installed key space (original column name)
     if (ks != qq->key_space.end()) {
-      // it must hold every value of the batch's dictionaries: the batch's merged keys are a subset
-      const MergedKeyColumn& K = ks->second;
-      if (K.type != m.type) return fail(PINOT_AMD_EINVAL, "key space of %s has the wrong type", g.c_str());
-      bool ok = true;
-      if (m.type == T_STRING) {
-        for (auto& v : m.vs) ok &= std::binary_search(K.vs.begin(), K.vs.end(), v, java_less);
-      } else if (is_float(m.type)) {
-        for (double v : m.vd) ok &= std::binary_search(K.vd.begin(), K.vd.end(), v, java_double_less);
-      } else {
-        for (int64_t v : m.vi) ok &= std::binary_search(K.vi.begin(), K.vi.end(), v);
+      // it must hold every value of the batch's dictionaries: the batch's merged keys are a subset (checked
+      // once per (batch key space, installed key space) pair: both are immutable)
+      const MergedKeyColumn& K = *ks->second;
+      if (K.type != m->type) return fail(PINOT_AMD_EINVAL, "key space of %s has the wrong type", g.c_str());
+      static std::mutex sub_mu;
+      static std::set<std::pair<uint64_t, uint64_t>> subsets;
+      bool known;
+      {
+        std::lock_guard<std::mutex> lk(sub_mu);
+        known = subsets.count({m->id, K.id}) != 0;
       }
-      if (!ok) return fail(PINOT_AMD_EINVAL, "key space of %s misses values of the segments' dictionaries", g.c_str());
-      m = K;
+      if (!known) {
+        bool ok = true;
+        if (m->type == T_STRING) {
+          for (auto& v : m->vs) ok &= std::binary_search(K.vs.begin(), K.vs.end(), v, java_less);
+        } else if (is_float(m->type)) {
+          for (double v : m->vd) ok &= std::binary_search(K.vd.begin(), K.vd.end(), v, java_double_less);
+        } else {
+          for (int64_t v : m->vi) ok &= std::binary_search(K.vi.begin(), K.vi.end(), v);
+        }
+        if (!ok) return fail(PINOT_AMD_EINVAL, "key space of %s misses values of the segments' dictionaries", g.c_str());
+        std::lock_guard<std::mutex> lk(sub_mu);
+        if (subsets.size() >= 65536) subsets.clear();
+        subsets.insert({m->id, K.id});
+      }
+      m = ks->second;
     }
     r->key_stride.push_back((int64_t)std::min(dense_keys, 9.0e18));
-    dense_keys *= (double)std::max<size_t>(m.size(), 1);
+    dense_keys *= (double)std::max<size_t>(m->size(), 1);
     r->keys.push_back(std::move(m));
   }
   // Matching docs per segment, counted once at plan time by a filter-only pass when a planning decision
@@ -2427,7 +2603,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   std::vector<int> seg_batch(n, 0);
   if (r->kind == PLAN_HASH) {
     std::vector<int64_t> sizes;
-    for (auto& m : r->keys) sizes.push_back((int64_t)std::max<size_t>(m.size(), 1));
+    for (auto& m : r->keys) sizes.push_back((int64_t)std::max<size_t>(m->size(), 1));
     pack_key_words(sizes, &r->pack_word, &r->pack_shift);
     r->pack_bits.clear();
     for (int64_t sz : sizes) r->pack_bits.push_back(bits_for(sz));
@@ -2444,11 +2620,29 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     // most PINOT_AMD_HASH_INIT_SLOTS slots and grow when groups overflow it (run_plan)
     double want = std::min(2.0 * fbound, (double)max_cap);
     if (!r->trim) want = std::min(want, (double)env_i64("PINOT_AMD_HASH_INIT_SLOTS", (int64_t)1 << 20));
-    const int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)want));
+    int64_t fcap = next_pow2(std::max<int64_t>(64, (int64_t)want));
+    const double max_bytes = (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30);
     const double fbytes = bytes_of(fcap, r->nw);
-    if (fbytes > (double)env_i64("PINOT_AMD_HASH_FINAL_MAX_BYTES", (int64_t)64 << 30))
+    if (fbytes > max_bytes)
       return fail(PINOT_AMD_EUNSUPPORTED, "group table of %lld slots (%.1f GB) exceeds PINOT_AMD_HASH_FINAL_MAX_BYTES",
                   (long long)fcap, fbytes / 1e9);
+    if (!r->trim) {
+      // growth ceiling: 2 x the group bound as a power of two, within the slot index range and the byte budget
+      int64_t ceil_cap = std::min<int64_t>(max_cap, next_pow2(std::max<int64_t>(64, (int64_t)std::min(2.0 * fbound, (double)max_cap))));
+      while (ceil_cap > 64 && bytes_of(ceil_cap, r->nw) > max_bytes) ceil_cap >>= 1;
+      r->fcap_ceiling = std::max(ceil_cap, fcap);
+      // an earlier execution of the same query shape over the same segments settled on a capacity: start there
+      std::string ck = preds_signature(Q.preds) + "\x1c";
+      for (size_t j = 0; j < Q.group_by.size(); ++j) ck += Q.group_by[j] + ":" + std::to_string(r->keys[j]->id) + ",";
+      ck += "\x1c";
+      for (auto* sg : segs) ck += std::to_string(sg->uid) + "." + std::to_string(sg->gen) + ",";
+      r->cap_key = ck;
+      const int64_t known = known_hash_capacity(ck);
+      if (known > 0 && !env_is("PINOT_AMD_HASH_CAP_CACHE", "0")) {
+        fcap = std::min(std::max(fcap, known), r->fcap_ceiling);
+        r->cap_known = true;
+      }
+    }
     r->fcap = fcap;
     if (r->trim) {
       // scan tables keyed by (key, segment), one batch of segments at a time
@@ -2498,15 +2692,11 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     for (size_t j = 0; j < Q.group_by.size(); ++j) {
       const Column& c = *segs[si]->cols.at(Q.group_by[j]);
-      std::vector<int32_t> rm;
-      remap_for(c, r->keys[j], &rm);
-      bool identity = (int64_t)rm.size() == (int64_t)r->keys[j].size();
-      for (size_t d = 0; identity && d < rm.size(); ++d) identity = rm[d] == (int32_t)d;
-      if (!identity) {
-        auto buf = std::make_unique<DevBuf>();
-        if (int rc = buf->alloc_copy(rm.data(), rm.size() * 4, 64)) return rc;
+      std::shared_ptr<DevBuf> buf;
+      if (int rc = cached_remap(segs[si], Q.group_by[j], c, *r->keys[j], &buf)) return rc;
+      if (buf) {
         ds.cols[slot_of(Q.group_by[j])].remap = (const int32_t*)buf->p;
-        r->owned.push_back(std::move(buf));
+        r->shared.push_back(std::move(buf));
       }
     }
     for (size_t k = 0; k < order.size(); ++k) {
@@ -2527,7 +2717,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       J.sel = (const int32_t*)il.sel->p;
       J.bitset = (unsigned long long*)il.bitset->p;
       J.num_docs = il.num_docs;
-      J.nwords = (int64_t)(il.bitset->n / 8);
+      J.nwords = std::max<int64_t>((il.num_docs + kTileDocs - 1) / kTileDocs, 1) * (kTileDocs / 64) + 8;  // not the slack
       J.sel_begin = total;
       J.nsel = il.nsel;
       J.grp = (const int32_t*)il.grp->p;
@@ -2827,6 +3017,27 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     const int64_t g = env_i64("PINOT_AMD_SCAN_GROUP", 4);
     base.sel_group = g >= 4 ? 4 : g >= 2 ? 2 : 1;
   }
+  // Narrow int64 LDS partials with tile groups: every segment's tile range is padded to a multiple of G and a
+  // block takes ceil(T' / (G x grid)) x G padded tiles, so the docs one block can add are bounded from the
+  // padded tile total (the G = 1 bound above used the unpadded one). If a sum's margin does not hold at that
+  // bound, the plan keeps one tile per step (the G = 1 bound, the same LDS layout).
+  if (base.lds && !base.select && q.nacc > 0 && base.sel_group > 1) {
+    auto docs_bound = [&](int64_t G) {
+      int64_t tp = 0;
+      for (auto* s : segs) tp += ((s->num_docs + kTileDocs - 1) / kTileDocs + G - 1) / G * G;
+      const int64_t mg = std::max<int64_t>(1, std::min<int64_t>(cus, tp / kPartSub));
+      return (__int128)((tp + G * mg - 1) / (G * mg) * G) * kTileDocs;
+    };
+    std::vector<int> before;
+    for (const JitAcc& a : base.accs) before.push_back(a.narrow);
+    set_narrow(docs_bound(base.sel_group));
+    bool same = true;
+    for (size_t i = 0; i < base.accs.size(); ++i) same &= base.accs[i].narrow == before[i];
+    if (!same) {
+      set_narrow(docs_bound(1));
+      base.sel_group = 1;
+    }
+  }
   {
     if (base.select && base.lds) {
       // gather blocks walk the selection vector grid-strided (padding included, matches unevenly spread
@@ -3113,6 +3324,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // narrow SSB select passes measured 1-3 % slower with them, the partitioned scatter 10 % slower
       jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") ||
                     (!env_is("PINOT_AMD_NT_LOADS", "0") && bpr >= 16.0 && !jp.partitioned && !jp.select);
+      jp.xcd_remap = env_is("PINOT_AMD_XCD_REMAP", "1");
+      jp.diag_admit_off = env_is("PINOT_AMD_DIAG_ADMIT_OFF", "1");
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);
@@ -3596,6 +3809,19 @@ static int check_overflow(pinot_amd_result* r) {
   hipStream_t st = r->stream;
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
+  if (r->ovf_pending) {
+    // an execution at a remembered capacity skipped its overflow check: if some doc found no slot after all,
+    // grow and run the plan again (it then checks, and grows further, itself)
+    r->ovf_pending = false;
+    if (c[3 * r->launches.size() + 1] != 0) {
+      bool grown = false;
+      if (int rc = grow_hash(r, &grown)) return rc;
+      if (grown) {
+        if (int rc = run_plan(r)) return rc;
+        if (int rc = read_counters(r, &c)) return rc;
+      }
+    }
+  }
   if (c[3 * r->launches.size() + 1] != 0)
     return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
                 (long long)c[3 * r->launches.size() + 1]);
@@ -3674,31 +3900,27 @@ static int compact_groups(pinot_amd_result* r) {
     if (int rc = oacc.ensure((size_t)ng * nacc * 8)) return rc;
     HIP_OK(launch_gather_groups((const int32_t*)idx.p, ng, T.keys, nwk, T.slots, T.acc, nacc, (uint64_t*)okeys.p,
                                 (uint64_t*)oacc.p, st));
-    HIP_OK(hipMemcpyAsync(r->ckeys.data(), okeys.p, r->ckeys.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(r->cacc.data(), oacc.p, r->cacc.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-  }
-  if (hash && ng > 1) {  // ascending global key: column ids compared from the last column to the first
-    const int G = r->num_group_by;
-    std::vector<std::vector<uint32_t>> ids((size_t)ng, std::vector<uint32_t>(G));
-    for (int64_t g = 0; g < ng; ++g)
-      for (int j = 0; j < G; ++j)
-        ids[g][j] = (uint32_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) &
-                               (((uint64_t)1 << r->pack_bits[j]) - 1));
-    std::vector<int64_t> perm((size_t)ng);
-    for (int64_t g = 0; g < ng; ++g) perm[g] = g;
-    std::sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) {
-      for (int j = G - 1; j >= 0; --j)
-        if (ids[a][j] != ids[b][j]) return ids[a][j] < ids[b][j];
-      return false;
-    });
-    std::vector<uint64_t> k2(r->ckeys.size()), a2(r->cacc.size());
-    for (int64_t i = 0; i < ng; ++i) {
-      std::copy_n(&r->ckeys[(size_t)perm[i] * nwk], nwk, &k2[(size_t)i * nwk]);
-      std::copy_n(&r->cacc[(size_t)perm[i] * nacc], nacc, &a2[(size_t)i * nacc]);
+    const void* src_keys = okeys.p;
+    const void* src_acc = oacc.p;
+    if (hash && ng > 1) {
+      // ascending global key (column ids compared from the last column to the first) = the packed key words
+      // as one integer, word nwk - 1 most significant: a stable LSD radix sort over the words on the device
+      // (derive.hip), then the sorted rows cross PCIe. (A host sort of 1.34M two-column keys took ~0.4 s.)
+      std::vector<int> word_bits(nwk, 1);
+      for (int j = 0; j < r->num_group_by; ++j)
+        word_bits[r->pack_word[j]] = std::max(word_bits[r->pack_word[j]], r->pack_shift[j] + r->pack_bits[j]);
+      DevBuf &sk = r->c_skeys, &sa = r->c_sacc, &ss = r->c_sscratch;
+      if (int rc = sk.ensure((size_t)ng * nwk * 8)) return rc;
+      if (int rc = sa.ensure((size_t)ng * nacc * 8)) return rc;
+      if (int rc = ss.ensure(sort_rows_scratch(ng))) return rc;
+      HIP_OK(sort_rows_by_key((const uint64_t*)okeys.p, nwk, word_bits.data(), (const uint64_t*)oacc.p, nacc, ng, ss.p,
+                              (uint64_t*)sk.p, (uint64_t*)sa.p, st));
+      src_keys = sk.p;
+      src_acc = sa.p;
     }
-    r->ckeys.swap(k2);
-    r->cacc.swap(a2);
+    HIP_OK(hipMemcpyAsync(r->ckeys.data(), src_keys, r->ckeys.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(r->cacc.data(), src_acc, r->cacc.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
   }
   if (int rc = server_trim(r)) return rc;
   r->compacted = true;
@@ -3791,7 +4013,7 @@ static int64_t group_key_id(const pinot_amd_result* r, int64_t g, int j) {
     const int nwk = r->merged ? r->mnw : r->nw;
     return (int64_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) & (((uint64_t)1 << r->pack_bits[j]) - 1));
   }
-  const int64_t sz = (int64_t)std::max<size_t>(r->keys[j].size(), 1);
+  const int64_t sz = (int64_t)std::max<size_t>(r->keys[j]->size(), 1);
   return ((int64_t)r->ckeys[(size_t)g] / std::max<int64_t>(r->key_stride[j], 1)) % sz;
 }
 
@@ -3898,7 +4120,7 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
     if (h_keys) {
       int64_t rem = hash ? 0 : (int64_t)r->ckeys[(size_t)g];
       for (int j = 0; j < r->num_group_by; ++j) {
-        const MergedKeyColumn& m = r->keys[j];
+        const MergedKeyColumn& m = *r->keys[j];
         int64_t id;
         if (hash) {
           id = (int64_t)((r->ckeys[(size_t)g * nwk + r->pack_word[j]] >> r->pack_shift[j]) & (((uint64_t)1 << r->pack_bits[j]) - 1));
@@ -3977,7 +4199,7 @@ int pinot_amd_result_fetch_intermediate(pinot_amd_result* r, int64_t cap, double
 
 const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t id) {
   if (!r || j < 0 || j >= r->num_group_by) return nullptr;
-  const MergedKeyColumn& m = r->keys[j];
+  const MergedKeyColumn& m = *r->keys[j];
   if (m.type != T_STRING || id < 0 || id >= (int64_t)m.vs.size()) return nullptr;
   return m.vs[id].c_str();
 }
@@ -4018,7 +4240,7 @@ static int key_pack(const pinot_amd_result* r, DevKeyPack* kp) {
   kp->ncols = r->num_group_by;
   if (kp->ncols > kMaxGroupCols) return fail(PINOT_AMD_EUNSUPPORTED, "export: %d group columns", kp->ncols);
   std::vector<int64_t> sizes;
-  for (int j = 0; j < kp->ncols; ++j) sizes.push_back((int64_t)std::max<size_t>(r->keys[j].size(), 1));
+  for (int j = 0; j < kp->ncols; ++j) sizes.push_back((int64_t)std::max<size_t>(r->keys[j]->size(), 1));
   std::vector<int> word, shift;
   pack_key_words(sizes, &word, &shift);  // the hash plan's packing
   for (int j = 0; j < kp->ncols; ++j) {

@@ -146,6 +146,13 @@ struct JitPlan {
   int wsel_words = 4;  // word-level select: 64-doc words per lane and step (4 or 8; 16 words are one tile)
   int sel_group = 1;   // tile-level select: 1024-doc tiles per loop step (1, 2 or 4; each segment's tile
                        // range in the launch padded to a multiple of it)
+  // XCD-aware tile ranges: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one), so the
+  // physical index is remapped to a logical one that gives each XCD one contiguous eighth of the launch's
+  // tiles -- its blocks then share the few segments' per-segment tables (admission bitmaps) in their L2
+  bool xcd_remap = false;
+  // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
+  // results; isolates the lookup's traffic in A/B profiles)
+  bool diag_admit_off = false;
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);

@@ -99,7 +99,7 @@ def _reduce_gathered(g, ops):
     return out
 
 
-def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_max_bytes: int = 1 << 20) -> None:
+def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_max_bytes: int = 1 << 20) -> int:
     """In-place merge across ranks of a [len(ops), num_keys] int64 tensor of accumulator words.
 
     ops per row: 0 = int64 sum, 1 = fp64 sum (words are double bits), 2/3 = min/max of the
@@ -109,19 +109,21 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_ma
     Tables up to gather_max_bytes: ONE all-gather of the whole table, reduced locally per row kind
     (a latency-bound exchange: one collective instead of one per reduction kind). Larger tables: one
     all-reduce per reduction kind (integer sums incl. the limbs of 128-bit rows in one int64 SUM, double
-    sums in one fp64 SUM, one MIN, one MAX), each moving ~2x the table per rank on a ring."""
+    sums in one fp64 SUM, one MIN, one MAX), each moving ~2x the table per rank on a ring.
+    Returns the bytes this rank put into the collectives."""
     import torch
     import torch.distributed as dist
     t = table.view(len(ops), num_keys)
     ops = list(ops)
     world = dist.get_world_size(group)
     if world == 1:
-        return
+        return 0
     if t.numel() * 8 <= gather_max_bytes:
         parts = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(parts, t.contiguous(), group=group)
         t.copy_(_reduce_gathered(torch.stack(parts), ops))
-        return
+        return t.numel() * 8
+    nbytes = 0
     i64 = [i for i, op in enumerate(ops) if op == OP_SUM_I64]
     i128 = [i for i, op in enumerate(ops) if op == OP_SUM_I128]
     f64 = [i for i, op in enumerate(ops) if op == OP_SUM_F64]
@@ -129,6 +131,7 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_ma
     parts += [_limbs(t[i], t[i + 1]) for i in i128]
     if parts:
         buf = torch.cat(parts).contiguous()
+        nbytes += buf.numel() * 8
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
         if i64:
             t[i64] = buf[:len(i64)]
@@ -138,14 +141,17 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_ma
             t[i + 1] = hi
     if f64:
         f = t[f64].contiguous().view(torch.float64)
+        nbytes += f.numel() * 8
         dist.all_reduce(f, op=dist.ReduceOp.SUM, group=group)
         t[f64] = f.view(torch.int64)
     for op, rop in ((OP_MIN, dist.ReduceOp.MIN), (OP_MAX, dist.ReduceOp.MAX)):
         rows = [i for i, o in enumerate(ops) if o == op]
         if rows:
             s_ = (t[rows] ^ SIGN).contiguous()
+            nbytes += s_.numel() * 8
             dist.all_reduce(s_, op=rop, group=group)
             t[rows] = s_ ^ SIGN
+    return nbytes
 
 
 class _DeviceWords:
@@ -170,7 +176,12 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
     still run the same collectives.
 
     `stream`: the stream the result was executed on; torch's current stream waits for it first.
-    `scratch` is unused (kept for callers)."""
+    `scratch`: None, or the dict an earlier merge_result of the SAME result object returned. The agreement
+    (the flag all-reduce and its host read) is a property of the plan, which re-executions over the same
+    immutable segments do not change: with the scratch of an earlier merge of this result the ranks skip it,
+    so a dense merge enqueues its collectives without a host synchronisation. scratch["stats"] describes the
+    last merge: its path ("dense-gather" / "dense-allreduce" / "by-value") and the bytes this rank put into
+    the collectives."""
     import torch
     import torch.distributed as dist
     cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
@@ -183,25 +194,32 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
     world = dist.get_world_size(group)
     if world == 1:
         return scratch
-    # DISTINCTCOUNT folds (group key, value) groups whose value column is not in the dense key space
-    local_by_value = hasattr(result, "results") or any(not p.has_dense_table() for p in parts)
-    reached = any(_limit_reached(p) for p in parts)
-    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    flag = torch.tensor([1 if local_by_value else 0, 1 if reached else 0], dtype=torch.int64, device=dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    by_value, reached_any = (bool(x) for x in flag.tolist())
+    if not isinstance(scratch, dict) or scratch.get("result") is not result:
+        # DISTINCTCOUNT folds (group key, value) groups whose value column is not in the dense key space
+        local_by_value = hasattr(result, "results") or any(not p.has_dense_table() for p in parts)
+        reached = any(_limit_reached(p) for p in parts)
+        dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        flag = torch.tensor([1 if local_by_value else 0, 1 if reached else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        by_value, reached_any = (bool(x) for x in flag.tolist())
+        scratch = {"result": result, "by_value": by_value, "reached": reached_any}
+    by_value, reached_any = scratch["by_value"], scratch["reached"]
+    stats = {"path": None, "bytes": 0}
     for p in parts:
         if hasattr(p, "set_merged_limit_reached"):
             p.set_merged_limit_reached(reached_any)
         if by_value and _grouped(p):
-            merge_by_value(p, group, cur, root)
+            stats["path"] = "by-value"
+            stats["bytes"] += merge_by_value(p, group, cur, root)
             continue
         ops, nk, ptrs = p.accumulators()
         if not ops:
             continue
         table = torch.as_tensor(_DeviceWords(ptrs[0], len(ops) * nk), device="cuda")
         assert table.data_ptr() == ptrs[0], "zero-copy view of the accumulator table failed"
-        merge_tables(table, ops, nk, group, gather_max_bytes)
+        stats["bytes"] += merge_tables(table, ops, nk, group, gather_max_bytes)
+        stats["path"] = stats["path"] or ("dense-gather" if len(ops) * nk * 8 <= gather_max_bytes else "dense-allreduce")
+    scratch["stats"] = stats
     return scratch
 
 
@@ -245,24 +263,28 @@ def merge_by_value(p, group=None, stream=None, root=None):
     """GroupByDataTableReducer's merge (GroupByDataTableReducer.java:258) across ranks, partitioned by key:
     export_groups -> all-to-all by key owner -> merge_groups of this rank's share (each group's partials
     meet on one rank, so 1/N of the rows per rank) -> the merged shares, disjoint, all-gathered (or
-    gathered on `root`) -> merge_groups again, which only inserts them."""
+    gathered on `root`) -> merge_groups again, which only inserts them. Returns the bytes this rank put into
+    the collectives (its exported rows, then its merged share)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     keys, acc = p.export_groups(stream=stream)
     kw = keys.shape[1]
     rows = torch.cat([keys, acc], dim=1)
+    nbytes = rows.numel() * 8
     mine = exchange_rows(rows, key_owner(keys, world), group)
     p.merge_groups(mine[:, :kw].contiguous(), mine[:, kw:].contiguous(), stream=stream)
     mk, ma = p.export_groups(stream=stream)
     share = torch.cat([mk, ma], dim=1)
+    nbytes += share.numel() * 8
     if root is None:
         allr = gather_rows(share, group)
     else:
         allr = gather_rows_to(share, root, group)
         if dist.get_rank(group) != root:
-            return
+            return nbytes
     p.merge_groups(allr[:, :kw].contiguous(), allr[:, kw:].contiguous(), stream=stream)
+    return nbytes
 
 
 def gather_rows(rows, group=None, return_counts: bool = False):

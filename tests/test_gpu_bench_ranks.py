@@ -29,3 +29,9 @@ def test_two_rank_bench_line(workload):
     # the whole job's rows: 2 ranks x 2 segments x 1M rows per step
     assert d["config"]["rows_per_gpu"] == 2_000_000
     assert d["value"] > 0 and d["ms_per_step"] > 0
+    # the merge's own share of a step and its bytes per rank (a scaling curve names its bottleneck)
+    m = d["merge"]
+    assert m["path"] in ("dense-gather", "dense-allreduce", "by-value")
+    assert m["bytes_per_rank"] > 0 and m["ms_events"] >= 0 and m["ms_wall_synchronized"] > 0
+    if workload == "highcard":  # 1M groups x 4 accumulator kinds: far above the 1 MiB gather threshold
+        assert m["path"] == "dense-allreduce"
