@@ -163,6 +163,32 @@ def server_table(qc, groups: dict) -> dict:
     return {k: groups[k] for k in ordered[:trim]}
 
 
+def segment_trim(qc, per_segment: list) -> dict:
+    """The segments' own trim, then the combine's merge of what they keep (GroupByOperator.java:157-175): a
+    segment holding more groups than trimSize keeps its top trimSize by the ORDER BY (TableResizer). Under a
+    safe trim -- ORDER BY expressions = GROUP BY expressions as sets, no HAVING (QueryContext.java:746-747) --
+    trimSize = LIMIT (QueryContext.calculateEffectiveSegmentGroupTrimSize, :568-580); otherwise no segment
+    trims here (minSegmentGroupTrimSize <= 0, the default: CommonConstants.java:1436). Groups outside the
+    global top LIMIT can thus carry partial results (only the segments whose top LIMIT they made).
+    per_segment: one {key: [partials]} dict per segment. Returns the combined {key: [partials]}."""
+    targets = qc.order_by_targets() if qc.order_by else []
+    safe = bool(targets) and all(kind == 0 for kind, _, _ in targets) and \
+        sorted({idx for _, idx, _ in targets}) == list(range(len(qc.group_by)))
+    out = {}
+    for groups in per_segment:
+        keep = list(groups)
+        if safe and qc.limit > 0 and len(groups) > qc.limit:
+            def sk(k):
+                return tuple(_value_order(k[idx]) if asc else _Desc(_value_order(k[idx])) for _, idx, asc in targets)
+            keep = sorted(groups, key=sk)[:qc.limit]
+        for k in keep:
+            if k not in out:
+                out[k] = list(groups[k])
+            else:
+                out[k] = [merge(a.func, x, y) for a, x, y in zip(qc.aggregations, out[k], groups[k])]
+    return out
+
+
 class _Desc:
     """Reverses the order of a sort key component (descending ORDER BY)."""
     __slots__ = ("v",)

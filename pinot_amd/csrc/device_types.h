@@ -195,6 +195,11 @@ struct DevQuery {
   unsigned long long* seen_n;
   int64_t seen_cap;
   unsigned long long* admit_flag;  // numGroupsLimitReached (the sequential admission pass sets it)
+  // segment-level safe trim (JitPlan::seg_ord): per segment (key_seg) the ORDER BY rank of its LIMIT-th
+  // group (~0: the segment keeps every group), and the presence bitmaps over ranks (seg_words words each)
+  const unsigned long long* seg_cut;
+  unsigned long long* seg_bits;
+  int64_t seg_words;
 };
 
 }  // namespace pamd

@@ -46,6 +46,8 @@ hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const
                         int64_t* bstar, int64_t* rank, unsigned long long* bitmap, int64_t* dstar,
                         unsigned long long* limit_reached, int phase, uint32_t* admit, int64_t words, hipStream_t st);
 hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st);
+hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
+                          unsigned long long* cut, hipStream_t st);
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
                                 hipStream_t st);
@@ -1209,6 +1211,8 @@ struct Launch {
   // launch's segments cut to their prefixes), or over whole segments (d_segs) when a prefix saw too few keys
   JitKernel* jit_fd = nullptr;
   JitKernel* jit_as = nullptr;  // the sequential admission (key spaces that fit LDS), one block per segment
+  JitKernel* jit_sp = nullptr;  // segment-level safe trim: the presence pass over ORDER BY ranks
+  int sp_grid = 1;
   DevBuf d_fd_segs;
   DevQuery fd_q{};
   int fd_grid = 1, fd_full_grid = 1;
@@ -1286,6 +1290,12 @@ struct pinot_amd_result {
   // matching docId of every key seen in its prefix, the list of those keys, and the admission bitmaps
   bool admit = false;
   DevBuf a_first, a_seen, a_seen_n, a_bits, a_hist, a_bbase, a_bstar, a_rank, a_bitmap, a_dstar;
+  // segment-level safe trim (JitPlan::seg_ord): per segment a presence bitmap over ORDER BY ranks (sp_words
+  // words) and the rank of its LIMIT-th group
+  bool seg_trim = false;
+  DevBuf sp_bits, sp_cut;
+  int64_t sp_words = 0;
+  int32_t sp_nsegs = 0;
   int64_t a_cap = 0, a_words = 0, a_buckets = 0, a_max_buckets = 0;
   std::vector<int64_t> a_prefix;       // docs of each segment the first pass reads
   std::vector<int64_t> a_docs;
@@ -2148,6 +2158,22 @@ static int run_plan(pinot_amd_result* r) {
   } else {
     if (r->admit)
       if (int rc = run_admission(r, limit_flag)) return rc;
+    if (r->seg_trim) {
+      // segment-level safe trim: each segment's groups marked by ORDER BY rank, then its LIMIT-th rank
+      HIP_OK(hipMemsetAsync(r->sp_bits.p, 0, r->sp_bits.n, st));
+      for (auto& L : r->launches) {
+        if (L.q.total_tiles == 0) continue;
+        const DevSegment* sg = (const DevSegment*)L.d_segs.p;
+        uint64_t* table = nullptr;
+        uint64_t* const* bits = nullptr;
+        unsigned long long* matched = nullptr;
+        DevHash h{};
+        void* args[] = {(void*)&sg, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&L.part, (void*)&h};
+        HIP_OK(hipModuleLaunchKernel(L.jit_sp->fn, (unsigned)L.sp_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+      }
+      HIP_OK(launch_seg_cut((const unsigned long long*)r->sp_bits.p, r->sp_words, r->sp_nsegs, r->srv_limit,
+                            (unsigned long long*)r->sp_cut.p, st));
+    }
     if (r->q.nacc > 0) HIP_OK(launch_init_acc((uint64_t*)r->acc.p, r->q, r->q.num_keys, st));
     DevHash H{};
     for (size_t li = 0; li < nl; ++li)
@@ -2446,8 +2472,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   r->limit_possible = limit_possible;
   // Safe trim with LIMIT >= sortAggregateLimitThreshold and no serverReturnFinalResult: every segment keeps its
   // top LIMIT groups by the ORDER BY (GroupByOperator.java:146-182, QueryContext.java:568-580) and the combine
-  // table keeps the top trimSize of their union, so groups past the global top LIMIT carry partial results. A
-  // segment that cannot hold more than LIMIT groups trims nothing; a segment-level trim is not restated here.
+  // table keeps the top trimSize of their union, so groups past the global top LIMIT carry partial results.
+  // Restated on dense key spaces (seg_trim): each segment's groups are marked in a presence bitmap over their
+  // ORDER BY ranks, the rank of its LIMIT-th group is the segment's cutoff, and the aggregation keeps only the
+  // docs whose group ranks within it. A segment that cannot hold more than LIMIT groups trims nothing. (Below
+  // the threshold, and with serverReturnFinalResult, the segments trim too, but the LIMIT groups the server
+  // keeps are exact either way: server_trim.)
+  bool seg_trim = false;
   if (r->srv_safe && r->srv_limit >= 0 && r->srv_limit >= r->srv_sort_threshold && !r->srv_final && !filter_only &&
       !Q.group_by.empty()) {
     auto over = [&]() {
@@ -2459,9 +2490,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (int rc = probe_matched()) return rc;
       for (int si = 0; si < n; ++si) seg_bound[si] = std::min(seg_bound[si], seg_matched[si]);
     }
-    if (over())
+    seg_trim = over() && !env_is("PINOT_AMD_SEG_TRIM", "0");
+    if (over() && !seg_trim)
       return fail(PINOT_AMD_EUNSUPPORTED, "server result limit: a segment-level safe trim (ORDER BY = GROUP BY, "
-                                          "LIMIT %lld >= sortAggregateLimitThreshold %lld) would drop groups",
+                                          "LIMIT %lld >= sortAggregateLimitThreshold %lld) disabled by PINOT_AMD_SEG_TRIM=0",
                   (long long)r->srv_limit, (long long)r->srv_sort_threshold);
   }
   // admission prefixes (dense trimming): the docs of segment si that should hold numGroupsLimit distinct
@@ -2589,6 +2621,28 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     r->kind = PLAN_DENSE;
   }
   if (r->admit) admit_prefixes();
+  std::vector<JitPlan::OrdCol> seg_ord;
+  if (seg_trim) {
+    if (r->kind != PLAN_DENSE)
+      return fail(PINOT_AMD_EUNSUPPORTED, "server result limit: a segment-level safe trim (LIMIT %lld >= "
+                                          "sortAggregateLimitThreshold %lld) over a key space beyond the dense cap",
+                  (long long)r->srv_limit, (long long)r->srv_sort_threshold);
+    // ORDER BY rank of a dense key: the first ORDER BY column most significant, DESC columns flipped
+    std::vector<std::pair<int, int>> ocols;  // (group column, ascending), first occurrence of each column
+    for (const auto& ob : r->srv_order)
+      if (std::none_of(ocols.begin(), ocols.end(), [&](const std::pair<int, int>& c) { return c.first == ob.index; }))
+        ocols.push_back({ob.index, ob.asc});
+    int64_t run = 1;
+    for (size_t o = ocols.size(); o-- > 0;) {
+      const int j = ocols[o].first;
+      const int64_t size = (int64_t)std::max<size_t>(r->keys[j]->size(), 1);
+      seg_ord.insert(seg_ord.begin(), JitPlan::OrdCol{std::max<int64_t>(r->key_stride[j], 1), size, run,
+                                                      ocols[o].second ? 0 : 1});
+      run *= size;
+    }
+    r->sp_words = (run + 63) / 64;
+    r->seg_trim = true;
+  }
   if (r->trim) {
     r->fd_acc = nacc;
     if (int rc = push_acc({-1, ACC_FIRST_DOC, 0, -1, 0})) return rc;
@@ -2761,6 +2815,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     base.accs.push_back({q.acc_op[a], acc_req[a].slot, acc_req[a].expr, acc_req[a].slot2, acc_req[a].nan_skip});
   base.num_keys = num_keys;
   base.admit = r->admit;
+  base.seg_ord = seg_ord;
   base.bitset = filter_only;
   base.aggregate = q.nacc > 0;
   int cus = 256;
@@ -2927,7 +2982,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const char* sel_env = getenv("PINOT_AMD_SELECT");
   // (a partitioned plan qualifies too: when its filter keeps few docs, the gather adds them straight into
   // the HBM table, where the partitioned plan would hand over to a fused direct-atomic scan of every row)
-  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit &&
+  const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit && !r->seg_trim &&
                             (r->kind == PLAN_DENSE || r->kind == PLAN_HASH || r->kind == PLAN_PARTITIONED) &&
                             !env_is("PINOT_AMD_SELECT_PARTITIONED", base.partitioned ? "0" : "-") &&
                             !(sel_env && !strcmp(sel_env, "never"));
@@ -3324,7 +3379,11 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // narrow SSB select passes measured 1-3 % slower with them, the partitioned scatter 10 % slower
       jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") ||
                     (!env_is("PINOT_AMD_NT_LOADS", "0") && bpr >= 16.0 && !jp.partitioned && !jp.select);
-      jp.xcd_remap = env_is("PINOT_AMD_XCD_REMAP", "1");
+      // XCD-aware tile ranges where blocks read per-segment tables beside the columns: the admission bitmaps
+      // (128 KiB per segment for configs[3]) thrashed each XCD's L2 when its blocks spanned every segment
+      // (default-limit configs[3] scatter: 20.1 -> 8.8 GB fetched per 400M rows, 4.87 -> 4.15 ms per plan;
+      // profiles/r05/pmc_hcdef_xcd.txt). PINOT_AMD_XCD_REMAP=0|1 pins it.
+      jp.xcd_remap = env_is("PINOT_AMD_XCD_REMAP", "1") || (jp.admit && !env_is("PINOT_AMD_XCD_REMAP", "0"));
       jp.diag_admit_off = env_is("PINOT_AMD_DIAG_ADMIT_OFF", "1");
     }
     if (jp.partitioned) {
@@ -3410,6 +3469,26 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nf, L.jit_fd->fn, kBlock, 0) != hipSuccess || nf < 1) nf = 1;
       L.fd_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, ftiles));
       L.fd_full_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, tiles));
+    }
+    if (r->seg_trim) {
+      // the segment-level safe trim's presence pass: the launch's filter (+ numGroupsLimit admission) and group
+      // key, each matching doc's ORDER BY rank marked in its segment's bitmap
+      JitPlan js = jp;
+      js.segpres = true;
+      js.lds = js.partitioned = js.select = js.word_select = js.atomic_gate = js.sample = js.part_sampled = false;
+      js.aggregate = false;
+      js.scan_nsub = 1;
+      js.sel_group = 1;
+      js.vals.clear();
+      js.val_bits.clear();
+      js.val_off.clear();
+      js.rec_bytes = js.stage_cap = js.nparts = js.key_shift = 0;
+      for (auto& lf : js.leaves) lf.lds_words = lf.lut = 0;
+      L.jit_sp = jit_get(js, &r->jit_status);
+      if (!L.jit_sp) return fail(PINOT_AMD_EUNSUPPORTED, "presence kernel unavailable: %s", r->jit_status.c_str());
+      int ns = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, L.jit_sp->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
+      L.sp_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, tiles));
     }
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
     L.shmem = jp.lds && !jp.partitioned ? (size_t)lds_bytes : jp.hash_lds ? (size_t)hash_lds_bytes : 0;
@@ -3668,11 +3747,27 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
     }
   }
+  if (r->seg_trim) {
+    r->sp_nsegs = n;
+    if (int rc = r->sp_bits.alloc((size_t)n * (size_t)r->sp_words * 8)) return rc;
+    if (int rc = r->sp_cut.alloc((size_t)n * 8)) return rc;
+    for (auto& L : r->launches) {
+      L.q.seg_cut = (const unsigned long long*)r->sp_cut.p;
+      L.q.seg_bits = (unsigned long long*)r->sp_bits.p;
+      L.q.seg_words = r->sp_words;
+    }
+  }
   clk.mark("jit_alloc");
   HIP_OK(hipEventCreate(&r->ev0));
   HIP_OK(hipEventCreate(&r->ev1));
+  const bool cap_from_cache = r->cap_known;
   if (int rc = run_plan(r)) return rc;
   clk.mark("launch");
+  if (r->kind == PLAN_HASH && !r->trim) {  // diagnostics: the table's slots, and whether an earlier execution sized it
+    char b[96];
+    snprintf(b, sizeof(b), ";hash_slots=%lld;hash_slots_remembered=%d", (long long)r->fcap, cap_from_cache ? 1 : 0);
+    r->plan_timing += b;
+  }
   *out = res.release();
   return 0;
 }

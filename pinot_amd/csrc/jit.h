@@ -153,6 +153,14 @@ struct JitPlan {
   // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
   // results; isolates the lookup's traffic in A/B profiles)
   bool diag_admit_off = false;
+  // Segment-level safe trim (GroupByOperator.java:157-175 with QueryContext's effective trim size = LIMIT):
+  // a dense key K's rank in the ORDER BY order is ord(K) = sum over the ORDER BY columns of id' x ostride,
+  // id = (K / stride) % size (the GROUP BY column's merged id), id' = size - 1 - id for DESC. Non-empty: the
+  // aggregation keeps a doc only when ord(key) <= DevQuery::seg_cut[segment] (each segment's top-LIMIT
+  // cutoff); segpres: instead of aggregating, set bit ord(key) of the segment's presence bitmap
+  struct OrdCol { int64_t stride, size, ostride; int flip; };
+  std::vector<OrdCol> seg_ord;
+  bool segpres = false;
 };
 // record layout of a partitioned plan (fills val_off / rec_bytes from vals and val_bits)
 void jit_layout_records(JitPlan* p);

@@ -347,6 +347,49 @@ __global__ void presence_bitset_kernel(const uint64_t* count, int64_t n, unsigne
   }
 }
 
+// Segment-level safe trim (GroupByOperator.java:157-175: a segment holding more than trimSize = LIMIT groups
+// keeps its top LIMIT by the ORDER BY): block s finds the ORDER BY rank of segment s's LIMIT-th group in its
+// presence bitmap over ranks -- per-thread popcounts over contiguous word runs, a block prefix, then the
+// thread whose run holds the LIMIT-th set bit walks it. cut[s] = that rank, or ~0 when the segment holds
+// <= LIMIT groups (nothing trimmed).
+__global__ void __launch_bounds__(1024) seg_cut_kernel(const unsigned long long* bits, int64_t words, int64_t limit,
+                                                       unsigned long long* cut) {
+  __shared__ long long pre[1024];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const unsigned long long* b = bits + (int64_t)s * words;
+  const int64_t per = (words + 1023) / 1024;
+  const int64_t w0 = min(words, (int64_t)tid * per), w1 = min(words, w0 + per);
+  long long c = 0;
+  for (int64_t w = w0; w < w1; ++w) c += __popcll(b[w]);
+  pre[tid] = c;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive prefix (Hillis-Steele)
+    const long long y = tid >= o ? pre[tid - o] : 0;
+    __syncthreads();
+    pre[tid] += y;
+    __syncthreads();
+  }
+  const long long total = pre[1023], ex = pre[tid] - c;
+  if (total <= limit) {
+    if (tid == 0) cut[s] = ~0ull;
+    return;
+  }
+  const long long want = limit - 1;  // 0-based index of the LIMIT-th group
+  if (ex <= want && want < ex + c) {
+    long long r = want - ex;
+    for (int64_t w = w0; w < w1; ++w) {
+      unsigned long long x = b[w];
+      const long long pc = __popcll(x);
+      if (r < pc) {
+        for (long long i = 0; i < r; ++i) x &= x - 1ull;  // drop the r lowest set bits
+        cut[s] = (unsigned long long)(w * 64 + __ffsll((long long)x) - 1);
+        return;
+      }
+      r -= pc;
+    }
+  }
+}
+
 // gather the compacted groups: key words (hash tables) and every accumulator word, row-major
 __global__ void gather_groups_kernel(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                      int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys,
@@ -1390,6 +1433,13 @@ hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int 
                              const int64_t* dstar, unsigned long long* overflow, hipStream_t st) {
   hipLaunchKernelGGL(hash_merge_kernel, dim3(grid_cap(scap, kBlock, 8192)), dim3(kBlock), 0, st, skeys, scap, nw, has_seg,
                      sacc, fkeys, fcap, facc, q, fd_acc, dstar, overflow);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
+                          unsigned long long* cut, hipStream_t st) {
+  if (nsegs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(seg_cut_kernel, dim3((unsigned)nsegs), dim3(1024), 0, st, bits, words, limit, cut);
   return hipGetLastError();
 }
 

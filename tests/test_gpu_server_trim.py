@@ -60,24 +60,81 @@ def test_server_table_vs_oracle(qi, plan, monkeypatch):
         assert list(got) == list(exp)
 
 
-def test_segment_level_safe_trim_is_refused(monkeypatch):
-    """LIMIT >= sortAggregateLimitThreshold under a safe trim: each segment would keep only its top LIMIT
-    groups (GroupByOperator.java:146-182); the library refuses rather than returning other groups."""
+SEG_TRIM_QUERIES = [
+    # safe trim (ORDER BY = GROUP BY) with LIMIT >= sortAggregateLimitThreshold: each segment keeps its top LIMIT
+    # groups (GroupByOperator.java:157-175), the combine table the top max(5 x LIMIT, minServerGroupTrimSize) of
+    # what they kept -- groups past the global top LIMIT carry the partials of the segments that kept them
+    "SET sortAggregateLimitThreshold = 5; SET minServerGroupTrimSize = 50; SELECT d0, COUNT(*), SUM(r_long) FROM t "
+    "GROUP BY d0 ORDER BY d0 LIMIT 8",
+    "SET sortAggregateLimitThreshold = 5; SET minServerGroupTrimSize = 200; SELECT d0, d1, COUNT(*), MIN(r_double), "
+    "AVG(r_int) FROM t WHERE r_int > 0 GROUP BY d0, d1 ORDER BY d1 DESC, d0 LIMIT 20",
+    "SET sortAggregateLimitThreshold = 10; SET minServerGroupTrimSize = -1; SELECT d1, d0, MAX(r_long) FROM t "
+    "GROUP BY d1, d0 ORDER BY d0 DESC, d1 DESC LIMIT 30",
+    # and with numGroupsLimit trimming first (each segment admits its first 500 groups, then trims to LIMIT)
+    "SET numGroupsLimit = 500; SET sortAggregateLimitThreshold = 5; SET minServerGroupTrimSize = 100; "
+    "SELECT d0, d1, COUNT(*) FROM t GROUP BY d0, d1 ORDER BY d0, d1 LIMIT 12",
+]
+
+
+@pytest.mark.parametrize("plan", ["auto", "partitioned"])
+@pytest.mark.parametrize("qi", range(len(SEG_TRIM_QUERIES)))
+def test_segment_level_safe_trim_vs_oracle(qi, plan, monkeypatch):
+    """The segment-level safe trim on the device (a presence pass over ORDER BY ranks, each segment's LIMIT-th
+    rank as its cutoff, the aggregation keeping the docs within it) against the oracle's restatement: every
+    segment trimmed to its top LIMIT by the ORDER BY (oracle_reduce.segment_trim), then the combine table."""
     import torch
     assert torch.cuda.is_available()
-    from pinot_amd import _lib
+    from oracle_reduce import segment_trim
+    from pinot_amd import engine as E
+    if plan == "partitioned":  # the key space leaves the LDS: the partitioned count / scatter passes trim
+        monkeypatch.setenv("PINOT_AMD_WIDE_LDS", "0")
+    rng = np.random.default_rng(90 + qi)
+    bufs = [random_segment(rng, 25_000 + 3_000 * i, name=f"sg{i}", bits_cards=(300, 37)) for i in range(3)]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = SEG_TRIM_QUERIES[qi]
+    qc = parse_sql(q)
+    res = E.ServerQueryExecutor(server_trim=True).execute(qc, segs)
+    got = res.groups()
+    oq = oracle.parse_sql(q)
+    per_seg = [oracle.execute(q, [b])[1] for b in bufs]
+    assert max(len(g) for g in per_seg) > qc.limit  # some segment trims
+    exp = server_table(oq, segment_trim(oq, per_seg))
+    _, full = oracle.execute(q, bufs)
+    assert exp != server_table(oq, full)  # the segment trim changes the server's result
+    assert len(got) == len(exp)
+    assert_same_groups(got, exp, set())
+    assert list(got) == list(exp)
+    if plan == "partitioned" and len(qc.group_by) > 1:
+        assert "partitioned" in res.kernel_info()
+
+
+def test_segment_level_safe_trim_untrimmed_segments():
+    """No segment can hold more than LIMIT groups: nothing to trim (the plan takes no presence pass)."""
+    import torch
+    assert torch.cuda.is_available()
     from pinot_amd import engine as E
     rng = np.random.default_rng(7)
     bufs = [random_segment(rng, 20_000, name="sf0", bits_cards=(300, 37))]
     segs = [E.ImmutableSegment(b) for b in bufs]
-    q = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY d0 LIMIT 5"
-    with pytest.raises(_lib.PinotAmdError, match="safe trim"):
-        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
-    # no segment can hold more than LIMIT groups: nothing to trim, accepted
     q2 = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t WHERE d0 < 3 GROUP BY d0 ORDER BY d0 LIMIT 5"
     got = E.ServerQueryExecutor(server_trim=True).execute(q2, segs).groups()
     _, full = oracle.execute(q2, bufs)
     assert got == server_table(oracle.parse_sql(q2), full)
+
+
+def test_segment_level_safe_trim_hash_plan_refused(monkeypatch):
+    """A hash-table plan (key space past the dense cap) does not restate the segment-level trim: refused."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import _lib
+    from pinot_amd import engine as E
+    monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    rng = np.random.default_rng(8)
+    bufs = [random_segment(rng, 20_000, name="sh0", bits_cards=(300, 37))]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY d0 LIMIT 5"
+    with pytest.raises(_lib.PinotAmdError, match="segment-level safe trim"):
+        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
 
 
 def test_ssb_server_table_vs_oracle():

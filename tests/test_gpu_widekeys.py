@@ -31,6 +31,7 @@ def wide():
                          ids=["lds", "lds64", "nolds", "grow", "grow-lds128"])
 def test_widekeys_hash_plan_vs_oracle(wide, env, monkeypatch):
     E, bufs, segs, exp = wide
+    monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")  # every case sizes (and grows) its own table
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     res = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
@@ -41,3 +42,58 @@ def test_widekeys_hash_plan_vs_oracle(wide, env, monkeypatch):
     assert sum(v[0] for v in got.values()) == res.num_docs_matched()
     res.execute_again()  # a re-execution (the grown table is kept) gives the same groups
     assert res.groups() == exp
+
+
+def test_widekeys_reissued_query_starts_at_the_grown_capacity(wide, monkeypatch):
+    """A query executed again through a fresh result (a new pinot_amd_execute, as a server re-issuing it) starts at
+    the capacity the first execution grew to, without the overflow check's host synchronisation -- and the
+    groups are the same."""
+    E, bufs, segs, exp = wide
+    monkeypatch.setenv("PINOT_AMD_HASH_INIT_SLOTS", "64")
+    r1 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    t1 = r1.plan_timing()
+    assert r1.groups() == exp
+    r2 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    t2 = r2.plan_timing()
+    assert t2["hash_slots_remembered"] == 1 and t2["hash_slots"] >= t1["hash_slots"] > 64, (t1, t2)
+    assert r2.groups() == exp
+    r2.execute_again()
+    assert r2.groups() == exp
+
+
+def test_widekeys_remembered_capacity_overflow_settled_at_fetch(wide, monkeypatch):
+    """An execution at a remembered capacity skips the overflow check; if docs then found no slot (here: probe
+    chains cut to 32 slots after the capacity was settled with 512), reading the groups grows the table and runs
+    the plan again -- the groups are exact either way."""
+    E, bufs, segs, exp = wide
+    monkeypatch.setenv("PINOT_AMD_HASH_INIT_SLOTS", "64")
+    r1 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    assert r1.groups() == exp
+    monkeypatch.setenv("PINOT_AMD_HASH_MAX_PROBE", "32")
+    r2 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    assert r2.plan_timing()["hash_slots_remembered"] == 1
+    assert r2.groups() == exp
+
+
+def test_hash_growth_lands_on_the_ceiling(monkeypatch):
+    """Growth is 4x per step but stops at the plan's ceiling (2 x its group bound as a power of two): from 64 slots
+    a table whose ceiling is 2^13 ends there (64 -> 256 -> 1024 -> 4096 -> 8192) instead of overshooting to 16384
+    (advisor); 4000 docs over an 11100-key space hold ~3300 groups, too many for 4096 slots at 64-slot chains."""
+    import numpy as np
+    import torch
+    assert torch.cuda.is_available()
+    from helpers import random_segment
+    from pinot_amd import engine as E
+    monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")
+    monkeypatch.setenv("PINOT_AMD_HASH_INIT_SLOTS", "64")
+    monkeypatch.setenv("PINOT_AMD_HASH_MAX_PROBE", "64")
+    monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    rng = np.random.default_rng(3)
+    bufs = [random_segment(rng, 4_000, name="hg0", bits_cards=(300, 37))]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = "SELECT d0, d1, COUNT(*), SUM(r_long) FROM t GROUP BY d0, d1"
+    res = E.ServerQueryExecutor().execute(q, segs)
+    _, exp = oracle.execute(q, bufs)
+    got = res.groups()
+    assert len(got) == len(exp) > 3000 and got == exp
+    assert res.plan_timing()["hash_slots"] == 8192
