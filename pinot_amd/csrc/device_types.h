@@ -158,7 +158,20 @@ struct DevHash {
   int64_t cap;                       // power of two
   unsigned long long* overflow;      // docs that found no free slot (the host grows the table or fails)
   int64_t max_probe;                 // > 0: a key gives up after this many slots (linear probing), 0: cap
+  // Second level of a hash plan with an LDS first level (JitPlan::hash_spill): a doc whose key finds no LDS
+  // slot is appended to its block's region as a spill record -- the key words, then one word per value
+  // accumulator (acc order, ACC_HI skipped: the int64 value, the double's bits, or the ordered MIN / MAX
+  // encoding) -- and counted in its key-hash partition (hash >> spill_shift). The spill passes (kernels.hip)
+  // then group the records by partition and aggregate each partition in LDS, so the tail keys reach the HBM
+  // table once per (partition chunk, key) instead of once per doc. Records past spill_cap take the HBM table.
+  unsigned long long* spill;         // grid x spill_cap records of spill_words words
+  int64_t spill_cap;
+  uint32_t* spill_cnt;               // per block: records appended (those past spill_cap counted too)
+  uint32_t* spill_hist;              // [partition * grid + block] records kept in the region
+  int32_t spill_shift;               // partitions = 2^(64 - spill_shift)
+  int32_t spill_words;
 };
+constexpr int kSpillMaxParts = 2048;  // spill partitions (the scan block's LDS histogram)
 
 // Group keys by value for the cross-rank merge (the broker reduce on the device): group column j's
 // merged id sits in bits [shift[j], shift[j] + bits) of key word word[j] (the hash plan's packing, <= 63

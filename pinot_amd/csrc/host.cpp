@@ -48,6 +48,9 @@ hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const
 hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st);
 hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
                           unsigned long long* cut, hipStream_t st);
+hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
+                               int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
+                               int agg_grid, int S, hipStream_t st);
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
                                 hipStream_t st);
@@ -1274,6 +1277,10 @@ struct pinot_amd_result {
   // reads the overflow counter (ovf_pending: check_overflow settles it when the groups are read)
   int64_t fcap_ceiling = 0;
   std::string cap_key;
+  // second level of the LDS-privatised hash plan (JitPlan::hash_spill, DevHash::spill)
+  DevBuf sp_rec, sp_sorted, sp_cnt, sp_hist, sp_offs, sp_pbeg;
+  int64_t spill_cap = 0, spill_grid = 0;
+  int spill_words = 0, spill_slots = 0, spill_agg_grid = 1;
   bool cap_known = false, ovf_pending = false;
   bool trim = false;                   // numGroupsLimit trimming (scan tables keyed by (key, segment))
   int64_t limit = 100000;
@@ -2115,11 +2122,28 @@ static int run_plan(pinot_amd_result* r) {
         // (below) instead of degrading into long serial CAS walks
         H.max_probe = env_i64("PINOT_AMD_HASH_MAX_PROBE", 512);
         table = (uint64_t*)r->acc.p;
+        if (r->spill_words > 0) {
+          // spill partitions: about 4096 table slots' worth of keys each (~1-2K groups), within the scan's
+          // LDS histogram; the second level's LDS table then holds a partition's keys
+          int lg = 6;
+          while (lg < 11 && ((int64_t)1 << lg) * 4096 < r->fcap) ++lg;
+          H.spill = (unsigned long long*)r->sp_rec.p;
+          H.spill_cap = r->spill_cap;
+          H.spill_cnt = (uint32_t*)r->sp_cnt.p;
+          H.spill_hist = (uint32_t*)r->sp_hist.p;
+          H.spill_shift = 64 - lg;
+          H.spill_words = r->spill_words;
+        }
       }
       H.overflow = overflow;
       for (size_t li = 0; li < nl; ++li)
-        if (r->launches[li].batch == b)
+        if (r->launches[li].batch == b) {
           if (int rc = launch_one(r, r->launches[li], li, table, H)) return rc;
+          if (!r->trim && r->spill_words > 0)
+            HIP_OK(launch_spill_passes(H, r->nw, r->launches[li].grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
+                                       (unsigned long long*)r->sp_sorted.p, r->q, (uint64_t*)r->acc.p, r->spill_agg_grid,
+                                       r->spill_slots, st));
+        }
       if (r->trim) {
         const int32_t nb = r->batch_nsegs[b];
         HIP_OK(hipMemsetAsync(r->t_hist.p, 0, (size_t)r->batch_buckets[b] * 4, st));
@@ -3121,12 +3145,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
     set_narrow((__int128)((all_tiles + min_grid - 1) / min_grid) * kTileDocs);
     const int64_t slot_bytes = (int64_t)(base.hash_words + lds_arrays()) * 8;
+    // second level: the LDS misses spilled as records and aggregated per key-hash partition (kernels.hip
+    // spill passes) instead of one HBM probe + atomics per doc; PINOT_AMD_HASH_SPILL=0 keeps the direct path
+    const bool spill = !env_is("PINOT_AMD_HASH_SPILL", "0");
+    const int64_t reserve = 1024 + (spill ? (int64_t)kSpillMaxParts * 4 + 16 : 0);
     // as many slots as the LDS holds beside the kernel's static LDS (counters), a multiple of 64
     int64_t S = env_i64("PINOT_AMD_HASH_LDS_SLOTS", 0);
-    if (S <= 0) S = std::min<int64_t>(8192, (lds_max - 1024) / slot_bytes);
+    if (S <= 0) S = std::min<int64_t>(8192, (lds_max - reserve) / slot_bytes);
     S = std::max<int64_t>(64, S / 64 * 64);
-    if (S * slot_bytes <= lds_max - 1024) {
+    if (S * slot_bytes <= lds_max - reserve) {
       base.hash_lds = (int)S;
+      base.hash_spill = spill;
       base.scan_nsub = kPartSub;
       hash_lds_bytes = S * slot_bytes;
     } else {
@@ -3399,6 +3428,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.part_sub = (int)env_i64("PINOT_AMD_PART_SUB", kPartSub);
       if (jp.part_sub != 1 && jp.part_sub != 2) jp.part_sub = kPartSub;
       const size_t stage_lds = (size_t)lds_max / (size_t)(kPartSub / jp.part_sub);
+      // admission plans: the segment's admission bitmap beside the staging (an LDS read per doc instead of a
+      // dependent global load; the scatter writes only the admitted docs' records, so a short staging serves)
+      jp.admit_lds = jp.admit && jp.part_sub == kPartSub && !env_is("PINOT_AMD_ADMIT_LDS", "0") &&
+                     jit_scatter_lds([&] { JitPlan t = jp; t.admit_lds = true; return t; }(), 4) <= stage_lds;
       int cap = 64;
       while (cap >= 4 && jit_scatter_lds(jp, cap) > stage_lds) --cap;
       jp.stage_cap = cap >= 4 ? cap : 0;
@@ -3680,6 +3713,32 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   if (r->kind == PLAN_HASH) {
     if (int rc = r->fkeys.alloc((size_t)r->nw * (size_t)r->fcap * 8)) return rc;
     if (int rc = r->acc.alloc((size_t)q.nacc * (size_t)r->fcap * 8)) return rc;
+    if (base.hash_spill) {
+      // spill regions: one per scan block, each holding up to the block's docs (every doc may miss), within
+      // PINOT_AMD_SPILL_BYTES (default 8 GiB) for the regions and as much for their partition-major copy;
+      // records past a region's capacity take the HBM table directly
+      int64_t gmax = 1, per_max = 1;
+      for (auto& L : r->launches) {
+        gmax = std::max<int64_t>(gmax, L.grid);
+        per_max = std::max<int64_t>(per_max, (L.q.total_tiles + L.grid - 1) / std::max(L.grid, 1));
+      }
+      int nval = 0;
+      for (const JitAcc& a : base.accs) nval += a.op != ACC_HI && a.op != ACC_FIRST_DOC;
+      r->spill_words = r->nw + nval;
+      const double budget = (double)env_i64("PINOT_AMD_SPILL_BYTES", (int64_t)8 << 30);
+      r->spill_cap = std::max<int64_t>(64, std::min<int64_t>(per_max * kTileDocs,
+                                                              (int64_t)(budget / ((double)gmax * r->spill_words * 8.0))));
+      r->spill_grid = gmax;
+      if (int rc = r->sp_rec.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
+      if (int rc = r->sp_sorted.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
+      if (int rc = r->sp_cnt.alloc((size_t)gmax * 4)) return rc;
+      if (int rc = r->sp_hist.alloc((size_t)kSpillMaxParts * (size_t)gmax * 4)) return rc;
+      if (int rc = r->sp_offs.alloc((size_t)kSpillMaxParts * (size_t)gmax * 8)) return rc;
+      if (int rc = r->sp_pbeg.alloc(((size_t)kSpillMaxParts + 1) * 8)) return rc;
+      // second-level LDS table: every slot's key words and accumulator arrays in one CU's LDS
+      r->spill_slots = (int)std::min<int64_t>(8192, (lds_max - 64) / ((int64_t)(r->nw + q.nacc) * 8));
+      r->spill_agg_grid = cus;
+    }
     if (r->trim) {
       const int64_t scap = *std::max_element(r->batch_cap.begin(), r->batch_cap.end());
       if (int rc = r->skeys.alloc((size_t)(r->nw + 1) * (size_t)scap * 8)) return rc;

@@ -129,6 +129,9 @@ struct JitPlan {
   // key that finds no LDS slot goes to the HBM table directly; the block flushes its occupied slots into
   // the HBM table at the end (one HBM probe + one atomic per accumulator per slot)
   int hash_lds = 0;
+  // with hash_lds: a key that finds no LDS slot is spilled (DevHash::spill: appended as a record and counted
+  // per key-hash partition) instead of probing the HBM table per doc
+  bool hash_spill = false;
   // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;
@@ -137,6 +140,10 @@ struct JitPlan {
   // aggregation (filter + group key -> atomicMin of the docId, keys seen first appended per segment)
   bool admit = false;
   bool firstdoc = false;
+  // partitioned scatter of an admission plan: the block's current segment's admission bitmap (num_keys / 8
+  // bytes) is held in LDS behind the staging, reloaded when the block's tiles cross into another segment, so
+  // a doc's admission test is an LDS read instead of a dependent global load per doc
+  bool admit_lds = false;
   // admitseq: the admission as one block per segment walking its prefix in doc order with the segment's
   // seen-key bitmap in LDS (key spaces of <= kAdmitSeqMaxKeys keys)
   bool admitseq = false;

@@ -336,6 +336,152 @@ __global__ void hash_merge_kernel(const unsigned long long* skeys, int64_t scap,
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Hash-plan second level (DevHash::spill, JitPlan::hash_spill): the scan's LDS first level keeps a skewed
+// key distribution's head on-die; the tail keys' docs were appended to their block's region as records (key
+// words, then one value word per value accumulator). Here they are grouped by key-hash partition (so every
+// record of a key meets in one partition) and each partition is aggregated in one block's LDS hash table,
+// then merged into the HBM table: one probe + one atomic per accumulator per (partition chunk, key) instead
+// of per doc -- the map-based holders' group-id lookups (DictionaryBasedGroupKeyGenerator.java:444-900)
+// with their per-doc random accesses moved on-die.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t key_hash_rt(const uint64_t* kw, int nw) {
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (int w = 0; w < nw; ++w) x = fmix64(x ^ kw[w]);
+  return x;
+}
+
+// block b moves its region's records to their partitions' places: part_begin[p] + offs[p * grid + b] + the
+// block's running count of partition p (LDS cursors)
+__global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
+                                                             const int64_t* part_begin, unsigned long long* out) {
+  extern __shared__ uint32_t cur[];
+  const int64_t b = blockIdx.x;
+  const int P = 1 << (64 - H.spill_shift), W = H.spill_words;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) cur[i] = 0u;
+  __syncthreads();
+  const int64_t n = min((int64_t)H.spill_cnt[b], H.spill_cap);
+  const unsigned long long* reg = H.spill + b * H.spill_cap * W;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const unsigned long long* r = reg + i * W;
+    uint64_t kw[kMaxKeyWords];
+    for (int w = 0; w < nw; ++w) kw[w] = r[w];
+    const int p = (int)(key_hash_rt(kw, nw) >> H.spill_shift);
+    const int64_t pos = part_begin[p] + offs[(int64_t)p * grid + b] + atomicAdd(&cur[p], 1u);
+    unsigned long long* o = out + pos * W;
+    for (int w = 0; w < W; ++w) o[w] = r[w];
+  }
+}
+
+// apply record value word v to accumulator a (op) at p / its high word ph: COUNT is applied by the caller
+__device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* ph, uint64_t v) {
+  if (op == ACC_SUM_I128) acc_apply(op, p, ph, v, (int64_t)v < 0 ? ~0ull : 0ull);
+  else acc_apply(op, p, ph, v, 0ull);
+}
+
+// Blocks take contiguous record ranges of the partition-major array; per partition a block meets, an LDS
+// open-addressing table of S slots (key words, then every accumulator array of the plan) aggregates the
+// records (a key that finds no slot within 64 probes goes to the HBM table directly), then every occupied
+// slot is merged into the HBM table (AggregationFunction.merge: counts and sums add, MIN / MAX by the ordered
+// encoding) and the table is cleared for the next partition.
+__global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long long* recs, const int64_t* part_begin,
+                                                         int P, int nw, int W, int S, DevQuery q, DevHash H,
+                                                         uint64_t* acc) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
+  unsigned long long* LK = lt;                         // nw x S key words
+  uint64_t* LA = (uint64_t*)(lt + (int64_t)nw * S);    // q.nacc x S accumulators
+  const int tid = threadIdx.x;
+  const int64_t total = part_begin[P];
+  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = min(total, r0 + per);
+  if (r0 >= r1) return;
+  int pi = 0;
+  {
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (part_begin[mid] <= r0) lo = mid; else hi = mid - 1;
+    }
+    pi = lo;
+  }
+  const int nacc = q.nacc;
+  while (r0 < r1) {
+    while (part_begin[pi + 1] <= r0) ++pi;
+    const int64_t pe = min(r1, part_begin[pi + 1]);
+    for (int i = tid; i < nw * S; i += blockDim.x) LK[i] = ~0ull;
+    for (int i = tid; i < nacc * S; i += blockDim.x) LA[i] = acc_identity(q.acc_op[i / S]);
+    __syncthreads();
+    for (int64_t i = r0 + tid; i < pe; i += blockDim.x) {
+      const unsigned long long* r = recs + i * W;
+      uint64_t kw[kMaxKeyWords];
+      for (int w = 0; w < nw; ++w) kw[w] = r[w];
+      const uint64_t x = key_hash_rt(kw, nw);
+      uint32_t s = (uint32_t)(((x & 0xFFFFFFFFull) * (uint64_t)(uint32_t)S) >> 32);
+      int ls = -1;
+      for (int n = 0; n < 64; ++n) {
+        bool ok = true;
+        for (int w = 0; w < nw && ok; ++w) {
+          unsigned long long* pw = LK + (uint32_t)w * (uint32_t)S + s;
+          unsigned long long c = *(volatile unsigned long long*)pw;
+          if (c == ~0ull) {
+            c = atomicCAS(pw, ~0ull, (unsigned long long)kw[w]);
+            if (c == ~0ull) c = kw[w];
+          }
+          ok = c == kw[w];
+        }
+        if (ok) {
+          ls = (int)s;
+          break;
+        }
+        s = s + 1u == (uint32_t)S ? 0u : s + 1u;
+      }
+      uint64_t* base;
+      int64_t stride;
+      if (ls >= 0) {
+        base = LA + ls;
+        stride = S;
+      } else {  // no LDS slot: straight into the HBM table
+        const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
+        if (slot < 0) {
+          atomicAdd(H.overflow, 1ull);
+          continue;
+        }
+        base = acc + slot;
+        stride = H.cap;
+      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(base), 1ull);
+      int j = nw;
+      for (int a = 1; a < nacc; ++a) {
+        const int32_t op = q.acc_op[a];
+        if (op == ACC_HI) continue;
+        spill_apply(op, base + (int64_t)a * stride, base + (int64_t)(a + 1 < nacc ? a + 1 : a) * stride, r[j++]);
+      }
+    }
+    __syncthreads();
+    for (int ls = tid; ls < S; ls += blockDim.x) {
+      const uint64_t c = LA[ls];
+      if (c == 0ull) continue;
+      uint64_t kw[kMaxKeyWords];
+      for (int w = 0; w < nw; ++w) kw[w] = LK[(int64_t)w * S + ls];
+      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
+      if (slot < 0) {
+        atomicAdd(H.overflow, c);
+        continue;
+      }
+      for (int a = 0; a < nacc; ++a) {
+        const uint64_t v = LA[(int64_t)a * S + ls];
+        const uint64_t vh = a + 1 < nacc ? LA[(int64_t)(a + 1) * S + ls] : 0ull;
+        acc_apply(q.acc_op[a], acc + (uint64_t)a * (uint64_t)H.cap + slot,
+                  acc + (uint64_t)(a + 1 < nacc ? a + 1 : a) * (uint64_t)H.cap + slot, v, vh);
+      }
+    }
+    __syncthreads();
+    r0 = pe;
+    ++pi;
+  }
+}
+
 // Result compaction (GroupKeyGenerator.getGroupKeys on the device): bit i of `bits` = table slot i
 // holds a group (its COUNT accumulator is non-zero); one wave ballot per 64 slots.
 __global__ void presence_bitset_kernel(const uint64_t* count, int64_t n, unsigned long long* bits) {
@@ -1433,6 +1579,23 @@ hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int 
                              const int64_t* dstar, unsigned long long* overflow, hipStream_t st) {
   hipLaunchKernelGGL(hash_merge_kernel, dim3(grid_cap(scap, kBlock, 8192)), dim3(kBlock), 0, st, skeys, scap, nw, has_seg,
                      sacc, fkeys, fcap, facc, q, fd_acc, dstar, overflow);
+  return hipGetLastError();
+}
+
+hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
+                               int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
+                               int agg_grid, int S, hipStream_t st) {
+  (void)hist_unused;
+  const int P = 1 << (64 - H.spill_shift);
+  // offsets of (partition, block) runs, partition-major (the histogram the scan left in H.spill_hist)
+  hipLaunchKernelGGL(partition_row_scan_kernel, dim3((unsigned)P), dim3(kBlock), 0, st, H.spill_hist, grid, offs, part_begin);
+  hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, part_begin, (int64_t)P, part_begin + P);
+  hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)grid), dim3(1024), (size_t)P * 4, st, H, nw, grid,
+                     (const int64_t*)offs, (const int64_t*)part_begin, sorted);
+  const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
+  (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, (const unsigned long long*)sorted,
+                     (const int64_t*)part_begin, P, nw, H.spill_words, S, q, H, acc);
   return hipGetLastError();
 }
 
