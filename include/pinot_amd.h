@@ -218,10 +218,18 @@ int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t 
  * no HAVING the table keeps LIMIT groups, GroupByUtils.java:134-139) and sortAggregateLimitThreshold. With
  * ORDER BY keys = GROUP BY keys (safe trim, QueryContext.java:568-580,746-747) and LIMIT below the threshold,
  * Pinot's sorted combine (CombinePlanNode.java:150-154) keeps the top LIMIT groups, exact; at or above it each
- * segment keeps its top LIMIT groups (GroupByOperator.java:146-182) -- execute then returns EUNSUPPORTED when
- * some segment could hold more than LIMIT groups (that segment-level trim is not restated). */
+ * segment keeps its top LIMIT groups by the ORDER BY (GroupByOperator.java:157-175) and the combine table the
+ * top trimSize of their union -- restated for dense key spaces (a presence pass over ORDER BY ranks, each
+ * segment's LIMIT-th rank as the cutoff its docs are aggregated within); over a hash-table key space execute
+ * returns EUNSUPPORTED when some segment could hold more than LIMIT groups. */
 int pinot_amd_query_set_server_options(pinot_amd_query* q, int32_t server_return_final_result,
                                        int64_t sort_aggregate_limit_threshold);
+/* QueryOptions minSegmentGroupTrimSize (default -1: CommonConstants.java:1436). With ORDER BY not equal to the
+ * GROUP BY keys (an unsafe trim) and a positive value, each segment would keep its top max(value, 5 x LIMIT)
+ * groups by the ORDER BY, aggregation values included (QueryContext.java:575-578): that trim is not restated,
+ * so execute returns EUNSUPPORTED when some segment could hold more groups than that. Under a safe trim the
+ * segment trim size is LIMIT whatever this value (pinot_amd_query_set_server_options). */
+int pinot_amd_query_set_segment_trim(pinot_amd_query* q, int64_t min_segment_group_trim_size);
 /* ORDER BY key of the server table, in order of precedence: kind 0 = group-by column `index` (value
  * order), kind 1 = aggregation `index` (final value, Double.compare); ascending != 0 for ASC. */
 int pinot_amd_query_add_order_by(pinot_amd_query* q, int32_t kind, int32_t index, int32_t ascending);

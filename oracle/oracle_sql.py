@@ -62,6 +62,7 @@ class OQuery:
     limit: int
     num_groups_limit: int = 100_000
     min_server_group_trim_size: int = 5000
+    min_segment_group_trim_size: int = -1
     group_trim_threshold: int = 1_000_000
     server_return_final_result: bool = False
     sort_aggregate_limit_threshold: int = 10_000
@@ -362,6 +363,8 @@ def parse(sql: str) -> OQuery:
             q.num_groups_limit = int(v)
         elif k == "minservergrouptrimsize":
             q.min_server_group_trim_size = int(v)
+        elif k == "minsegmentgrouptrimsize":
+            q.min_segment_group_trim_size = int(v)
         elif k == "grouptrimthreshold":
             q.group_trim_threshold = int(v)
         elif k == "serverreturnfinalresult":

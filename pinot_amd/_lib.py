@@ -100,6 +100,7 @@ SIGNATURES = {
     "pinot_amd_query_set_result_limit": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64]),
     "pinot_amd_query_add_order_by": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32]),
     "pinot_amd_query_set_server_options": (C.c_int, [_P, C.c_int32, C.c_int64]),
+    "pinot_amd_query_set_segment_trim": (C.c_int, [_P, C.c_int64]),
     "pinot_amd_result_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "pinot_amd_result_kernel_info": (C.c_char_p, [_P]),
     "pinot_amd_result_algorithmic_bytes": (C.c_int, [_P, C.POINTER(C.c_double)]),

@@ -1017,6 +1017,7 @@ struct pinot_amd_query {
   // sortAggregateLimitThreshold (QueryContext.shouldSortAggregateUnderSafeTrim, default 10000)
   int server_final = 0;
   int64_t sort_agg_threshold = 10000;
+  int64_t min_seg_trim = -1;  // minSegmentGroupTrimSize
 };
 
 extern "C" {
@@ -1158,6 +1159,12 @@ int pinot_amd_query_set_server_options(pinot_amd_query* q, int32_t server_return
   if (!q || sort_aggregate_limit_threshold <= 0) return fail(PINOT_AMD_EINVAL, "set_server_options: bad arguments");
   q->server_final = server_return_final_result ? 1 : 0;
   q->sort_agg_threshold = sort_aggregate_limit_threshold;
+  return 0;
+}
+
+int pinot_amd_query_set_segment_trim(pinot_amd_query* q, int64_t min_segment_group_trim_size) {
+  if (!q) return fail(PINOT_AMD_EINVAL, "set_segment_trim: null query");
+  q->min_seg_trim = min_segment_group_trim_size;
   return 0;
 }
 
@@ -2519,6 +2526,24 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       return fail(PINOT_AMD_EUNSUPPORTED, "server result limit: a segment-level safe trim (ORDER BY = GROUP BY, "
                                           "LIMIT %lld >= sortAggregateLimitThreshold %lld) disabled by PINOT_AMD_SEG_TRIM=0",
                   (long long)r->srv_limit, (long long)r->srv_sort_threshold);
+  }
+  // Unsafe trim (ORDER BY other than the GROUP BY keys) with minSegmentGroupTrimSize > 0: each segment would keep
+  // its top max(minSegmentGroupTrimSize, 5 x LIMIT) groups by the ORDER BY, aggregation values included
+  // (QueryContext.java:575-578, GroupByOperator.java:157-175) -- not restated: refused when it would cut.
+  if (!r->srv_safe && !r->srv_order.empty() && Q.min_seg_trim > 0 && r->srv_limit >= 0 && !filter_only &&
+      !Q.group_by.empty()) {
+    const int64_t seg_keep = std::max<int64_t>(Q.min_seg_trim, 5 * r->srv_limit);
+    bool over = false;
+    for (int si = 0; si < n; ++si) over |= seg_bound[si] > seg_keep;
+    if (over && !Q.preds.empty() && seg_matched.empty()) {
+      if (int rc = probe_matched()) return rc;
+      over = false;
+      for (int si = 0; si < n; ++si) over |= std::min(seg_bound[si], seg_matched[si]) > seg_keep;
+    }
+    if (over)
+      return fail(PINOT_AMD_EUNSUPPORTED, "segment group trim: minSegmentGroupTrimSize %lld with an ORDER BY other than the "
+                                          "GROUP BY keys would trim segments to %lld groups (not restated)",
+                  (long long)Q.min_seg_trim, (long long)seg_keep);
   }
   // admission prefixes (dense trimming): the docs of segment si that should hold numGroupsLimit distinct
   // keys, twice the coupon-collector expectation for K uniform keys (K ln(K / (K - L)) matching docs,

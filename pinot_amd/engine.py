@@ -514,6 +514,7 @@ class ServerQueryExecutor:
                                                          qc.group_trim_threshold), "set_result_limit")
                 check(L.pinot_amd_query_set_server_options(qh, 1 if qc.server_return_final_result else 0,
                                                            qc.sort_aggregate_limit_threshold), "set_server_options")
+                check(L.pinot_amd_query_set_segment_trim(qh, qc.min_segment_group_trim_size), "set_segment_trim")
             native = []
             agg_slots = []
 

@@ -140,6 +140,7 @@ class QueryContext:
     num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT
     # the server combine table's trim options (QueryOptionsUtils: minServerGroupTrimSize, groupTrimThreshold)
     min_server_group_trim_size: int = 5000
+    min_segment_group_trim_size: int = -1  # QueryOptions minSegmentGroupTrimSize (CommonConstants.java:1436)
     group_trim_threshold: int = 1_000_000
     # serverReturnFinalResult, sortAggregateLimitThreshold (CommonConstants: default 10000)
     server_return_final_result: bool = False
@@ -433,8 +434,8 @@ def _query_options(sql: str):
 
 def parse_sql(sql: str) -> QueryContext:
     """Compile a Pinot SQL query of the supported subset into a QueryContext. The numGroupsLimit,
-    minServerGroupTrimSize, groupTrimThreshold, serverReturnFinalResult and sortAggregateLimitThreshold query
-    options (QueryOptionsUtils) are honoured; other options are ignored."""
+    minServerGroupTrimSize, groupTrimThreshold, serverReturnFinalResult, sortAggregateLimitThreshold and
+    minSegmentGroupTrimSize query options (QueryOptionsUtils) are honoured; other options are ignored."""
     sql, opts = _query_options(sql)
     qc = _Parser(sql).query()
     for k, v in opts.items():
@@ -448,6 +449,8 @@ def parse_sql(sql: str) -> QueryContext:
             qc.server_return_final_result = v.strip().lower() == "true"
         elif k.lower() == "sortaggregatelimitthreshold":
             qc.sort_aggregate_limit_threshold = int(v)
+        elif k.lower() == "minsegmentgrouptrimsize":
+            qc.min_segment_group_trim_size = int(v)
     return qc
 
 

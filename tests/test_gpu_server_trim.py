@@ -122,6 +122,26 @@ def test_segment_level_safe_trim_untrimmed_segments():
     assert got == server_table(oracle.parse_sql(q2), full)
 
 
+def test_unsafe_segment_trim_option_refused():
+    """minSegmentGroupTrimSize > 0 with an ORDER BY on an aggregation (an unsafe trim): each segment would keep its
+    top max(value, 5 x LIMIT) groups by aggregation values (QueryContext.java:575-578) -- not restated, refused when
+    a segment could hold more; with few enough groups per segment it cuts nothing and is accepted."""
+    import torch
+    assert torch.cuda.is_available()
+    from pinot_amd import _lib
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(9)
+    bufs = [random_segment(rng, 20_000, name="su0", bits_cards=(300, 37))]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = "SET minSegmentGroupTrimSize = 10; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY COUNT(*) DESC LIMIT 2"
+    with pytest.raises(_lib.PinotAmdError, match="minSegmentGroupTrimSize"):
+        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
+    q2 = "SET minSegmentGroupTrimSize = 1000; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY COUNT(*) DESC LIMIT 2"
+    got = E.ServerQueryExecutor(server_trim=True).execute(q2, segs).groups()
+    _, full = oracle.execute(q2, bufs)
+    assert list(got) == list(server_table(oracle.parse_sql(q2), full))
+
+
 def test_segment_level_safe_trim_hash_plan_refused(monkeypatch):
     """A hash-table plan (key space past the dense cap) does not restate the segment-level trim: refused."""
     import torch
