@@ -374,7 +374,9 @@ def main():
             matched_all = matched
         qc = parse_sql(query)
         # size-independent property: the merged group COUNTs add up to the docs that passed the filter
-        counts_first = bool(qc.aggregations) and qc.aggregations[0].func == "COUNT"
+        # (diagnostic knobs that deliberately break results skip it; their lines say so in config)
+        diag = sorted(k for k in os.environ if k.startswith("PINOT_AMD_DIAG_"))
+        counts_first = bool(qc.aggregations) and qc.aggregations[0].func == "COUNT" and not diag
         if qc.group_by and counts_first:
             # numGroupsLimit trimming drops the docs of groups a segment did not admit (they were scanned)
             total = sum(p[0] for p in groups.values())
@@ -435,6 +437,7 @@ def main():
                                    else "1 GPU",
                     "hbm_bytes_per_gpu": hbm,
                     "scan_kernel": res.kernel_info(),
+                    "diagnostic_knobs": diag or None,
                 },
                 "cold_ms": cold_ms,
                 "cached_plan_ms": plan_ms,

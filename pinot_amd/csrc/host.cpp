@@ -3439,6 +3439,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // profiles/r05/pmc_hcdef_xcd.txt). PINOT_AMD_XCD_REMAP=0|1 pins it.
       jp.xcd_remap = env_is("PINOT_AMD_XCD_REMAP", "1") || (jp.admit && !env_is("PINOT_AMD_XCD_REMAP", "0"));
       jp.diag_admit_off = env_is("PINOT_AMD_DIAG_ADMIT_OFF", "1");
+      if (jp.partitioned) {
+        const int64_t w = env_i64("PINOT_AMD_DIAG_REC_WRAP", 0);
+        jp.diag_rec_wrap = (w >= 4096 && (w & (w - 1)) == 0) ? w : 0;
+      }
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);

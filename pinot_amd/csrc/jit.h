@@ -160,6 +160,10 @@ struct JitPlan {
   // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
   // results; isolates the lookup's traffic in A/B profiles)
   bool diag_admit_off = false;
+  // diagnostics only (PINOT_AMD_DIAG_REC_WRAP = bytes, a power of two): the scatter's flushed records wrap around
+  // a buffer of that many bytes (wrong results; with a small wrap the record writes stay in the Infinity Cache,
+  // which measures what the record round trip through HBM costs the scatter)
+  int64_t diag_rec_wrap = 0;
   // Segment-level safe trim (GroupByOperator.java:157-175 with QueryContext's effective trim size = LIMIT):
   // a dense key K's rank in the ORDER BY order is ord(K) = sum over the ORDER BY columns of id' x ostride,
   // id = (K / stride) % size (the GROUP BY column's merged id), id' = size - 1 - id for DESC. Non-empty: the
