@@ -148,7 +148,7 @@ def committed_traffic(query: str, kernel_info: str, rows: int):
     gfx950 correction of MI355X_MICROARCH.md) + WRITE_SIZE, per row of the profiled run, scaled to `rows`.
     A record of another plan (a planner change since the pass) is not used: traffic is then None."""
     sha = query_sha1(query)
-    for rnd in ("r04", "r03"):
+    for rnd in ("r05", "r04", "r03"):
         pmc = os.path.join(ROOT, "profiles", rnd, "pmc_index.json")
         if not os.path.exists(pmc):
             continue
@@ -160,7 +160,7 @@ def committed_traffic(query: str, kernel_info: str, rows: int):
             t = (d["hbm_read_bytes"] + d["hbm_write_bytes"]) / d["rows"] * rows
             src = (f"profiles/{rnd}/pmc_index.json[{key}] (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE per execution of "
                    f"this query on plan {d.get('scan_kernel', '?')} over {d['rows']:.0f} rows, commit "
-                   f"{d.get('commit', '?')}, scaled per row; profiles/profile_{rnd}.sh)")
+                   f"{d.get('commit', '?')}, scaled per row; ROUND={rnd} profiles/profile.sh)")
             return t, src
     return None, None
 

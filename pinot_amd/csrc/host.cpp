@@ -122,32 +122,123 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // device buffers
 // ------------------------------------------------------------------------------------------------
+// Device blocks released by destroyed results are kept for the next execution instead of going back to
+// hipFree: a re-issued query shape allocates the same descriptors, bitset buffers and scratch again, and
+// hipMalloc / hipFree (which synchronises the device) cost tens of microseconds each -- hundreds of them per
+// plan on an inverted-index filter over 100 segments. Only pinot_amd_result_destroy releases into the
+// cache, after synchronising the result's stream, so a cached block is idle when it is handed out again.
+// Blocks up to kPoolMaxBlock bytes, PINOT_AMD_POOL_BYTES in total per device (default 1 GiB; 0 disables).
+struct DevPool {
+  static constexpr size_t kPoolMaxBlock = (size_t)256 << 20;
+  std::mutex mu;
+  std::map<int, std::multimap<size_t, void*>> free;  // device -> (block bytes -> block)
+  std::map<int, size_t> bytes;
+  size_t cap = 0;
+  DevPool() {
+    const char* e = getenv("PINOT_AMD_POOL_BYTES");
+    cap = e ? (size_t)strtoull(e, nullptr, 10) : ((size_t)1 << 30);
+  }
+  static size_t block_size(size_t n) {  // size classes: powers of two to 4 MiB, 1 MiB steps above
+    if (n <= 256) return 256;
+    if (n <= ((size_t)4 << 20)) {
+      size_t c = 512;
+      while (c < n) c <<= 1;
+      return c;
+    }
+    return (n + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+  }
+  void* take(size_t bsz) {
+    if (!cap || bsz > kPoolMaxBlock) return nullptr;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    auto& f = free[dev];
+    auto it = f.find(bsz);
+    if (it == f.end()) return nullptr;
+    void* p = it->second;
+    f.erase(it);
+    bytes[dev] -= bsz;
+    return p;
+  }
+  // false: not cached (the caller frees it)
+  bool put(void* p, size_t bsz) {
+    if (!cap || bsz > kPoolMaxBlock) return false;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    auto& f = free[dev];
+    size_t& b = bytes[dev];
+    while (b + bsz > cap && !f.empty()) {  // evict the largest cached blocks first
+      auto last = std::prev(f.end());
+      (void)hipFree(last->second);
+      b -= last->first;
+      f.erase(last);
+    }
+    if (b + bsz > cap) return false;
+    f.emplace(bsz, p);
+    b += bsz;
+    return true;
+  }
+};
+static DevPool& dev_pool() {
+  static DevPool* pool = new DevPool();  // never destroyed: blocks outlive static destruction order
+  return *pool;
+}
+// set by pinot_amd_result_destroy while the result's members are destroyed (its stream synchronised)
+static thread_local bool g_release_to_pool = false;
+
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
+  size_t bsz = 0;  // block bytes when the block is of a pool size class (0: an exact hipMalloc)
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  ~DevBuf() { release(); }
+  void release() {
+    if (p && !(g_release_to_pool && bsz && dev_pool().put(p, bsz))) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    bsz = 0;
+  }
+  int raw_alloc(size_t len) {
+    n = len;
+    const size_t want = len ? len : 1;
+    bsz = DevPool::block_size(want);
+    if (bsz <= DevPool::kPoolMaxBlock) {
+      if ((p = dev_pool().take(bsz))) return 0;
+      if (hipMalloc(&p, bsz) == hipSuccess) return 0;
+    }
+    bsz = 0;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", len);
+    }
+    return 0;
   }
   // allocate n bytes + pad (zeroed), copy `src` (len bytes) to the front
   int alloc_copy(const void* src, size_t len, size_t pad) {
-    n = len + pad;
-    if (hipMalloc(&p, n) != hipSuccess) return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
-    HIP_OK(hipMemset(p, 0, n));
+    release();
+    if (int rc = raw_alloc(len + pad)) return rc;
+    if (!pad) {
+      if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
+      else HIP_OK(hipMemset(p, 0, n));
+      return 0;
+    }
+    if (len + pad <= ((size_t)1 << 20)) {  // one copy of the bytes and their zero padding
+      std::vector<uint8_t> h(len + pad, 0);
+      if (len) memcpy(h.data(), src, len);
+      HIP_OK(hipMemcpy(p, h.data(), n, hipMemcpyHostToDevice));
+      return 0;
+    }
+    HIP_OK(hipMemset((uint8_t*)p + len, 0, pad));
     if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
     return 0;
   }
-  void reset() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
+  void reset() { release(); }
   int alloc(size_t len) {
-    n = len;
-    if (hipMalloc(&p, n ? n : 1) != hipSuccess) return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
-    return 0;
+    release();
+    return raw_alloc(len);
   }
   // at least len bytes, reusing the buffer when it is large enough (scratch kept across calls)
   int ensure(size_t len) {
@@ -246,6 +337,20 @@ struct Column {
   bool has_inv = false;
 };
 
+// A predicate leaf resolved on one segment (make_leaf_for_segment), kept on the segment: a re-issued filter
+// skips the dictionary lookups, the inverted-index container selection and the descriptor uploads (the
+// inverted-index leaves of configs[2]: 26-151 ms of host planning per execution over 100 segments).
+struct LeafCacheEntry {
+  DevLeaf L;
+  bool needs_slot = false;
+  std::vector<std::shared_ptr<DevBuf>> bufs;  // the device buffers the leaf points at (sets, descriptors)
+  bool inv = false;                           // inverted-index leaf: a docId bitset per execution
+  size_t bitset_alloc = 0;
+  DevBuf *sel = nullptr, *grp = nullptr, *psel = nullptr;
+  int32_t nsel = 0, nchunks = 0;
+  double alg_bytes = 0, bitset_bytes = 0;
+};
+
 struct pinot_amd_segment {
   std::string name;
   int64_t num_docs = 0;
@@ -256,6 +361,7 @@ struct pinot_amd_segment {
   // docs matching a filter (signature of its predicates -> count), counted once by the planner's
   // filter-only probe: the segment is immutable, so a filter's count never changes
   std::map<std::string, int64_t> match_cache;
+  std::map<std::string, std::shared_ptr<const LeafCacheEntry>> leaf_cache;  // guarded by g_leaf_mu
 };
 
 static bool is_float(int t) { return t == T_FLOAT || t == T_DOUBLE; }
@@ -1465,9 +1571,9 @@ static bool use_inverted_for(const Column& c, int64_t num_docs, const std::vecto
 // docId-bitset slack behind an inverted-index leaf's words (make_leaf_for_segment): 64 tiles
 constexpr size_t kBitsetSlackBytes = 64 * kTileDocs / 8;
 
-static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_segment* seg, const PredSpec& p,
-                                 const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
-                                 bool decoded_anyway) {
+static int make_leaf_uncached(pinot_amd_result* r, int si, const pinot_amd_segment* seg, const PredSpec& p,
+                              const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
+                              bool decoded_anyway) {
   memset(L, 0, sizeof(*L));
   L->slot = slot;
   L->clause = p.clause;
@@ -1664,6 +1770,82 @@ static int make_leaf_for_segment(pinot_amd_result* r, int si, const pinot_amd_se
   return 0;
 }
 
+static bool env_is(const char* name, const char* val);
+static std::mutex g_leaf_mu;  // guards every segment's leaf_cache
+constexpr size_t kLeafCacheMax = 256;  // entries per segment (cleared when full)
+
+// make_leaf_uncached through the segment's leaf cache. The key is everything the resolution reads: the
+// predicate, the slot, whether its column is decoded anyway, and the knobs of the inverted-index policy.
+static int make_leaf_for_segment(pinot_amd_result* r, int si, pinot_amd_segment* seg, const PredSpec& p,
+                                 const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
+                                 bool decoded_anyway) {
+  const bool use_cache = !env_is("PINOT_AMD_LEAF_CACHE", "0");
+  std::string key;
+  if (use_cache) {
+    const char* pol = getenv("PINOT_AMD_INV_POLICY");
+    key = preds_signature({p}) + "|" + std::to_string(slot) + "|" + (decoded_anyway ? "1" : "0") + "|" +
+          std::to_string(expand_group()) + "|" + (pol ? pol : "");
+    std::shared_ptr<const LeafCacheEntry> e;
+    {
+      std::lock_guard<std::mutex> g(g_leaf_mu);
+      auto it = seg->leaf_cache.find(key);
+      if (it != seg->leaf_cache.end()) e = it->second;
+    }
+    if (e) {
+      *L = e->L;
+      *needs_slot = e->needs_slot;
+      for (auto& b : e->bufs) r->shared.push_back(b);
+      if (e->inv) {
+        auto bs = std::make_unique<DevBuf>();
+        if (int rc = bs->alloc(e->bitset_alloc)) return rc;
+        L->bits = (const uint32_t*)bs->p;
+        r->inv_leaves.push_back({si, &c, bs.get(), e->sel, e->grp, e->nsel, e->nchunks, seg->num_docs, e->alg_bytes,
+                                 e->bitset_bytes, e->psel});
+        r->owned.push_back(std::move(bs));
+      }
+      return 0;
+    }
+  }
+  const size_t o0 = r->owned.size(), i0 = r->inv_leaves.size();
+  if (int rc = make_leaf_uncached(r, si, seg, p, c, slot, L, needs_slot, st, decoded_anyway)) return rc;
+  if (!use_cache) return 0;
+  auto e = std::make_shared<LeafCacheEntry>();
+  e->L = *L;
+  e->needs_slot = *needs_slot;
+  const DevBuf* bitset = nullptr;
+  if (r->inv_leaves.size() > i0) {
+    const auto& il = r->inv_leaves.back();
+    e->inv = true;
+    e->bitset_alloc = il.bitset->n;
+    e->sel = il.sel;
+    e->grp = il.grp;
+    e->psel = il.psel;
+    e->nsel = il.nsel;
+    e->nchunks = il.nchunks;
+    e->alg_bytes = il.alg_bytes;
+    e->bitset_bytes = il.bitset_bytes;
+    bitset = il.bitset;
+    HIP_OK(hipStreamSynchronize(st));  // the packed descriptors (launch_pack_sel) are read by later streams
+  }
+  // the leaf's descriptor buffers move to shared ownership (same objects: the pointers above stay valid);
+  // the per-execution docId bitset stays owned by this result
+  std::vector<std::unique_ptr<DevBuf>> keep;
+  for (size_t k = o0; k < r->owned.size(); ++k) {
+    if (r->owned[k].get() == bitset) {
+      keep.push_back(std::move(r->owned[k]));
+      continue;
+    }
+    std::shared_ptr<DevBuf> sb(r->owned[k].release());
+    e->bufs.push_back(sb);
+    r->shared.push_back(std::move(sb));
+  }
+  r->owned.resize(o0);
+  for (auto& k : keep) r->owned.push_back(std::move(k));
+  std::lock_guard<std::mutex> g(g_leaf_mu);
+  if (seg->leaf_cache.size() >= kLeafCacheMax) seg->leaf_cache.clear();
+  seg->leaf_cache[key] = std::move(e);
+  return 0;
+}
 
 // GROUP BY on a raw (no-dictionary) column: NoDictionarySingleColumnGroupKeyGenerator /
 // NoDictionaryMultiColumnGroupKeyGenerator (pinot-core/.../query/aggregation/groupby/
@@ -2640,6 +2822,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     r->agg_acc2.push_back(agg_req2[ai] < 0 ? 0 : req_acc[agg_req2[ai]]);
   }
 
+  clk.mark("accs");
   // ---- plan kind ----
   // dense table: mixed-radix keys over the merged dictionaries; hash table: key spaces beyond the
   // dense cap (DictionaryBasedGroupKeyGenerator's Int/Long/ArrayMapBasedHolder) and numGroupsLimit
@@ -2701,6 +2884,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const int64_t num_keys = r->kind == PLAN_HASH ? 0 : (int64_t)dense_keys;
   q.num_keys = num_keys;
 
+  clk.mark("plan_kind");
   // ---- hash plans: key packing and table sizes ----
   const int64_t table_budget = env_i64("PINOT_AMD_HASH_TABLE_BYTES", (int64_t)4 << 30);  // per trim scan table
   std::vector<int> seg_batch(n, 0);
@@ -2777,6 +2961,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
 
+  clk.mark("hash_sizes");
   // ---- device segments (one DevSegment per segment; tile_begin / key_seg set per launch) ----
   std::vector<DevSegment> hsegs(n);
   for (int si = 0; si < n; ++si) {
@@ -2846,6 +3031,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
 
+  clk.mark("dev_segs");
   // ---- plan-level kernel choices (shared by every launch) ----
   int lds_max = 0;
   {
@@ -3010,6 +3196,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     for (size_t j = 0; j < Q.group_by.size(); ++j) base.hash_pack.push_back({r->pack_word[j], r->pack_shift[j]});
   }
 
+  clk.mark("kernel_choices");
   // ---- selection-vector plan (late materialisation) ----
   // A selective filter over narrow rows: the select pass reads only the filter columns and appends the
   // matching docIds; the gather pass reads the group-by / aggregated columns of those docs only (64 B
@@ -3188,7 +3375,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
   }
 
-  clk.mark("plan");
+  clk.mark("select_plan");
   // ---- launches: segments of a batch grouped by shape (slot encodings and fixed-bit widths) ----
   const bool generic_bits = env_is("PINOT_AMD_GENERIC_BITS", "1");
   std::vector<int32_t> key_seg(n, 0);
@@ -3904,7 +4091,13 @@ int pinot_amd_execute_again(pinot_amd_result* r, void* stream) {
 }
 
 int pinot_amd_result_destroy(pinot_amd_result* r) {
+  if (!r) return 0;
+  // the result's work is finished before its blocks go to the device pool (a caller still reading a
+  // pinot_amd_result_bitset buffer on another stream must order that read before this call)
+  const bool idle = hipStreamSynchronize(r->stream) == hipSuccess;
+  g_release_to_pool = idle;
   delete r;
+  g_release_to_pool = false;
   return 0;
 }
 

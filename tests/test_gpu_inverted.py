@@ -78,3 +78,27 @@ def test_roaring_container_kinds(engine, q, monkeypatch):
     nm, og = oracle.execute(q, bufs)
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)
+
+
+def test_leaf_cache_reissued_filters(engine, inv_segments, monkeypatch):
+    """Predicate leaves resolved once per segment (the segment's leaf cache) serve re-issued filters: the
+    same queries interleaved, re-executed through fresh results while earlier results are still alive and
+    after they are destroyed (their blocks back in the device pool), each against the oracle."""
+    monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
+    bufs, segs = inv_segments
+    ex = engine.ServerQueryExecutor()
+    qs = [datagen.inverted_query(s) for s in datagen.INVERTED_SELECTIVITIES[:3]]
+    exp = {q: oracle.execute(q, bufs) for q in qs}
+    alive = []
+    for rnd in range(3):
+        for q in qs:
+            res = ex.execute(q, segs)
+            nm, og = exp[q]
+            assert res.num_docs_matched() == nm
+            assert_same_groups(res.groups(), og if nm else {(): og[()]}, {2})
+            if rnd == 1:
+                alive.append(res)  # held across the next round's executions of the same leaves
+            else:
+                res.destroy()
+    for res in alive:
+        res.destroy()
