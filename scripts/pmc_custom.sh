@@ -18,7 +18,7 @@ for f in glob.glob("gpurun_out/pmcc/p*/**/run_counter_collection.csv", recursive
     per = collections.defaultdict(float)
     for row in csv.DictReader(open(f)):
         k = row["Kernel_Name"]
-        if "pinot_" not in k:
+        if "pinot_" not in k and "spill_" not in k:
             continue
         per[(k, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
     for (k, d, c), v in per.items():
