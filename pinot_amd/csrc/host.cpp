@@ -1342,6 +1342,7 @@ struct pinot_amd_result {
   DevQuery q{};                  // plan-wide: nacc, acc_op, num_keys (dense)
   std::deque<Launch> launches;  // deque: Launch holds device buffers and is never moved
   std::vector<std::unique_ptr<DevBuf>> owned;  // leaf sets, remaps, bitsets
+  bool filter_gate = false;  // the fused scan loads key / value columns behind its filter (JitPlan::filter_gate)
   // inverted index leaves to (re)build each execution: (segment, leaf, container selection)
   struct InvLeaf {
     int seg;
@@ -3308,6 +3309,44 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     const int64_t g = env_i64("PINOT_AMD_SCAN_GROUP", 4);
     base.sel_group = g >= 4 ? 4 : g >= 2 ? 2 : 1;
   }
+  // Filter-gated value loads (JitPlan::filter_gate) for a fused dense scan: the filter columns load ahead and
+  // the group-key / value columns only for lanes with a matching doc. A lane holds 4 docs, so a 64-byte sector
+  // of a B-byte column (64 / B docs) is fetched when any of its docs matches: 1 - (1 - s)^(64 / B) of it at
+  // selectivity s (the segments' exact match counts). Chosen when the bytes it reads -- the filter columns, then
+  // the fetched share of every column read after the filter (a filter column that is also a key or value is
+  // read twice) -- are at most 3/4 of the fused scan's. PINOT_AMD_FILTER_GATE=0|1 pins it.
+  if (!base.select && r->kind == PLAN_DENSE && !base.partitioned && !r->admit && !filter_only && q.nacc > 0 && np > 0 &&
+      !env_is("PINOT_AMD_FILTER_GATE", "0")) {
+    bool ok = true;  // docId-bitset leaves gate through the inverted-index path instead
+    for (size_t k = 0; k < order.size() && ok; ++k)
+      for (int si = 0; si < n; ++si) ok &= hsegs[si].leaves[k].kind != LEAF_DOC_BITSET;
+    const bool forced = env_is("PINOT_AMD_FILTER_GATE", "1");
+    double fused_b = 0, filter_b = 0, value_b = 0;
+    for (int si = 0; si < n && ok; ++si)
+      for (int sl = 0; sl < nslots; ++sl) {
+        const double b = slot_bpr(hsegs[si].cols[sl]) * (double)segs[si]->num_docs;
+        fused_b += b;
+        if (leaf_slot[sl]) filter_b += b;
+        if (value_slot[sl]) value_b += b;
+      }
+    // worth a match-count probe only if the value columns could be skipped for a real share of the bytes
+    if (ok && (forced || filter_b + 0.1 * value_b <= 0.75 * fused_b)) {
+      if (int rc = probe_matched()) return rc;
+      double gated_b = 0;
+      for (int si = 0; si < n; ++si) {
+        const double docs = (double)std::max<int64_t>(segs[si]->num_docs, 1);
+        const double sel = std::min(1.0, (double)seg_matched[si] / docs);
+        for (int sl = 0; sl < nslots; ++sl) {
+          const double bpr = slot_bpr(hsegs[si].cols[sl]);
+          if (leaf_slot[sl]) gated_b += bpr * docs;
+          if (value_slot[sl] && bpr > 0) gated_b += bpr * docs * (1.0 - std::pow(1.0 - sel, 64.0 / bpr));
+        }
+      }
+      base.filter_gate = forced || gated_b <= 0.75 * fused_b;
+      r->filter_gate = base.filter_gate;
+      if (base.filter_gate) base.sel_group = 1;  // gated plans take one tile per step
+    }
+  }
   // Narrow int64 LDS partials with tile groups: every segment's tile range is padded to a multiple of G and a
   // block takes ceil(T' / (G x grid)) x G padded tiles, so the docs one block can add are bounded from the
   // padded tile total (the G = 1 bound above used the unpadded one). If a sum's margin does not hold at that
@@ -4160,6 +4199,7 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
       info += L.fused ? "-fwselect" : L.word_select ? "-wselect" : "-select";
       break;
     }
+  if (r->filter_gate) info += "+fgate";
   if (r->admit) {
     bool seq = !env_is("PINOT_AMD_ADMIT_SEQ", "0");
     for (auto& L : r->launches) seq &= L.jit_as != nullptr;

@@ -157,6 +157,11 @@ struct JitPlan {
   // physical index is remapped to a logical one that gives each XCD one contiguous eighth of the launch's
   // tiles -- its blocks then share the few segments' per-segment tables (admission bitmaps) in their L2
   bool xcd_remap = false;
+  // Filter-gated value loads (fused scans of selective filters): the filter columns of tile t + 2D are loaded
+  // ahead, the whole filter is evaluated D tiles ahead into a per-lane mask, and the group-key / value columns of
+  // that tile load only for lanes with a matching doc -- at a few percent selectivity most 64-byte sectors of
+  // the wide value columns are never fetched (late materialisation inside the scan, no selection vector)
+  bool filter_gate = false;
   // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
   // results; isolates the lookup's traffic in A/B profiles)
   bool diag_admit_off = false;

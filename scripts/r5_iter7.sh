@@ -8,5 +8,7 @@ SETS="FETCH_SIZE;WRITE_SIZE TCC_HIT_sum TCC_MISS_sum;$SQ" ARGS="--workload wide-
 cat gpurun_out/r5_pmc_wk.txt
 SETS="$SQ;SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA;FETCH_SIZE" ARGS="--workload ssb --segments 20 --query-index 11" timeout -k 10 600 bash scripts/pmc_custom.sh > gpurun_out/r5_pmc_q42.txt 2>&1 || { echo PMC_Q42_FAILED; tail -20 gpurun_out/r5_pmc_q42.txt; exit 1; }
 cat gpurun_out/r5_pmc_q42.txt
+SETS="$SQ;SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA" ARGS="--workload highcard --segments 40" timeout -k 10 600 bash scripts/pmc_custom.sh > gpurun_out/r5_pmc_hc.txt 2>&1 || { echo PMC_HC_FAILED; tail -20 gpurun_out/r5_pmc_hc.txt; exit 1; }
+cat gpurun_out/r5_pmc_hc.txt
 SETS="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" ARGS="--workload wide-keys --segments 40" timeout -k 10 300 bash scripts/pmc_custom.sh > gpurun_out/r5_pmc_wk_wrreq.txt 2>&1 || { echo PMC_WRREQ_FAILED; tail -5 gpurun_out/r5_pmc_wk_wrreq.txt; exit 1; }
 cat gpurun_out/r5_pmc_wk_wrreq.txt
