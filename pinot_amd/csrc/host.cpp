@@ -50,7 +50,7 @@ hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t
                           unsigned long long* cut, hipStream_t st);
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
-                               int agg_grid, int S, hipStream_t st);
+                               int agg_grid, int S, int sorted_scatter, hipStream_t st);
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
                                 hipStream_t st);
@@ -1319,6 +1319,7 @@ struct Launch {
   size_t shmem_sets = 0;  // LDS dictId sets of the scan / select pass (JitLeaf::lds_words)
   int gather_grid = 1, gather_threads = 256;
   double filter_bytes = 0, value_bpr = 0;  // select: filter columns over all docs; gathered bytes per match
+  bool fgate = false;  // filter-gated fused scan: filter columns over all docs, value bytes per match
   // partitioned: record size; sampled capacities (strided histogram instead of the count pass)
   int rec_bytes = 0;
   bool part_sampled = false;
@@ -2332,7 +2333,7 @@ static int run_plan(pinot_amd_result* r) {
           if (!r->trim && r->spill_words > 0)
             HIP_OK(launch_spill_passes(H, r->nw, r->launches[li].grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
                                        (unsigned long long*)r->sp_sorted.p, r->q, (uint64_t*)r->acc.p, r->spill_agg_grid,
-                                       r->spill_slots, st));
+                                       r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "1") ? 1 : 0, st));
         }
       if (r->trim) {
         const int32_t nb = r->batch_nsegs[b];
@@ -3709,6 +3710,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         if (jl.kinds != (1u << LEAF_DOC_BITSET) || jl.negate) gate[jl.clause] = 0;
       }
       for (int c = 0; c < nclauses; ++c) L.gated |= gate[c] && has[c];
+      if (jp.filter_gate) {  // filter columns of every doc, the key / value columns of the matching docs
+        L.fgate = true;
+        for (size_t k = 0; k < L.segs.size(); ++k)
+          for (int sl = 0; sl < nslots; ++sl) {
+            const double bpr = slot_bpr(ls[k].cols[sl]);
+            if (leaf_slot[sl]) L.filter_bytes += bpr * (double)ls[k].num_docs;
+            if (value_slot[sl] && k == 0) L.value_bpr += bpr;
+          }
+      }
       // gated plans: column loads D tiles ahead of their gate, gate words 2D ahead. Measured on the
       // inverted-index sweep, deeper pipelines only add registers (the gated loop is bound by its
       // per-tile overhead, not by load latency), so the row-width depth stays unless overridden.
@@ -4174,6 +4184,8 @@ int pinot_amd_result_algorithmic_bytes(pinot_amd_result* r, double* h_bytes) {
     if (L.select) {  // filter columns of every doc, the vector written and read, the gathered columns
       const double m = (double)c[3 * li];
       b += L.filter_bytes + m * (16.0 + L.value_bpr);
+    } else if (L.fgate) {
+      b += L.filter_bytes + (double)std::max(c[3 * li], c[3 * li + 2]) * L.value_bpr;
     } else if (!L.gated || L.docs == 0) {
       b += L.col_bytes;
     } else {  // gated: only the rows that pass the filter need their column bytes

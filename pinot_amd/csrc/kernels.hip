@@ -373,6 +373,76 @@ __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, 
   }
 }
 
+// LDS-sorted variant (PINOT_AMD_SPILL_SORT=1): the block counting-sorts chunks of C records of its region by
+// partition in LDS, then writes the chunk word by word in partition order -- consecutive lanes store
+// consecutive words of a partition's run, instead of one 8-byte store per lane and word into 64 scattered
+// runs. C = 1024 x per records (per = 1 or 2 per thread).
+__global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
+                                                                    const int64_t* part_begin, unsigned long long* out,
+                                                                    int per) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long sh_[];
+  __shared__ uint32_t wsum[16];
+  const int P = 1 << (64 - H.spill_shift), W = H.spill_words, C = 1024 * per;
+  unsigned long long* stage = sh_;                                // C x W words
+  long long* base = (long long*)(stage + (size_t)C * W);          // P: partition p's next output record
+  uint32_t* cnt = (uint32_t*)(base + P);                          // P: the chunk's records per partition
+  uint32_t* start = cnt + P;                                      // P: their exclusive prefix
+  uint16_t* pid = (uint16_t*)(start + P);                         // C: partition of each sorted slot
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t b = blockIdx.x;
+  for (int i = tid; i < P; i += 1024) base[i] = part_begin[i] + offs[(int64_t)i * grid + b];
+  const int64_t n = min((int64_t)H.spill_cnt[b], H.spill_cap);
+  const unsigned long long* reg = H.spill + b * H.spill_cap * W;
+  for (int64_t c0 = 0; c0 < n; c0 += C) {
+    const int m = (int)min((int64_t)C, n - c0);
+    for (int i = tid; i < P; i += 1024) cnt[i] = 0u;
+    __syncthreads();
+    int pr[2] = {-1, -1}, rk[2] = {0, 0};
+    for (int h = 0; h < per; ++h) {
+      const int i = tid + h * 1024;
+      if (i >= m) continue;
+      const unsigned long long* r = reg + (c0 + i) * W;
+      uint64_t kw[kMaxKeyWords];
+      for (int w = 0; w < nw; ++w) kw[w] = r[w];
+      pr[h] = (int)(key_hash_rt(kw, nw) >> H.spill_shift);
+      rk[h] = (int)atomicAdd(&cnt[pr[h]], 1u);
+    }
+    __syncthreads();
+    {  // exclusive prefix of the counts (P <= 2048: two entries per thread)
+      const int i0 = tid * 2;
+      const uint32_t a = i0 < P ? cnt[i0] : 0u, a2 = i0 + 1 < P ? cnt[i0 + 1] : 0u;
+      uint32_t x = a + a2;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wv] = x;
+      __syncthreads();
+      uint32_t off = 0;
+      for (int k = 0; k < wv; ++k) off += wsum[k];
+      const uint32_t ex = off + x - (a + a2);
+      if (i0 < P) start[i0] = ex;
+      if (i0 + 1 < P) start[i0 + 1] = ex + a;
+    }
+    __syncthreads();
+    for (int h = 0; h < per; ++h) {
+      if (pr[h] < 0) continue;
+      const int i = tid + h * 1024, pos = (int)start[pr[h]] + rk[h];
+      const unsigned long long* r = reg + (c0 + i) * W;
+      for (int w = 0; w < W; ++w) stage[(size_t)pos * W + w] = r[w];
+      pid[pos] = (uint16_t)pr[h];
+    }
+    __syncthreads();
+    for (int j = tid; j < m * W; j += 1024) {
+      const int pos = j / W, w = j - pos * W, p = pid[pos];
+      out[(size_t)(base[p] + (pos - (int)start[p])) * W + w] = stage[j];
+    }
+    __syncthreads();
+    for (int i = tid; i < P; i += 1024) base[i] += cnt[i];
+    __syncthreads();
+  }
+}
+
 // apply record value word v to accumulator a (op) at p / its high word ph: COUNT is applied by the caller
 __device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* ph, uint64_t v) {
   if (op == ACC_SUM_I128) acc_apply(op, p, ph, v, (int64_t)v < 0 ? ~0ull : 0ull);
@@ -1584,14 +1654,25 @@ hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int 
 
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
-                               int agg_grid, int S, hipStream_t st) {
+                               int agg_grid, int S, int sorted_scatter, hipStream_t st) {
   (void)hist_unused;
   const int P = 1 << (64 - H.spill_shift);
   // offsets of (partition, block) runs, partition-major (the histogram the scan left in H.spill_hist)
   hipLaunchKernelGGL(partition_row_scan_kernel, dim3((unsigned)P), dim3(kBlock), 0, st, H.spill_hist, grid, offs, part_begin);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, part_begin, (int64_t)P, part_begin + P);
-  hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)grid), dim3(1024), (size_t)P * 4, st, H, nw, grid,
-                     (const int64_t*)offs, (const int64_t*)part_begin, sorted);
+  const auto sorted_lds = [&](int per) {
+    return (size_t)1024 * per * H.spill_words * 8 + (size_t)P * (8 + 4 + 4) + (size_t)1024 * per * 2;
+  };
+  const int per = sorted_lds(2) <= (size_t)150 * 1024 ? 2 : 1;
+  if (sorted_scatter && sorted_lds(per) <= (size_t)150 * 1024) {
+    (void)hipFuncSetAttribute((const void*)spill_scatter_sorted_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sorted_lds(per));
+    hipLaunchKernelGGL(spill_scatter_sorted_kernel, dim3((unsigned)grid), dim3(1024), sorted_lds(per), st, H, nw, grid,
+                       (const int64_t*)offs, (const int64_t*)part_begin, sorted, per);
+  } else {
+    hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)grid), dim3(1024), (size_t)P * 4, st, H, nw, grid,
+                       (const int64_t*)offs, (const int64_t*)part_begin, sorted);
+  }
   const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
   (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, (const unsigned long long*)sorted,
