@@ -102,3 +102,30 @@ def test_leaf_cache_reissued_filters(engine, inv_segments, monkeypatch):
                 res.destroy()
     for res in alive:
         res.destroy()
+
+
+@pytest.mark.parametrize("plan", ["scan", "select"])
+@pytest.mark.parametrize("q", [
+    "SELECT COUNT(*), SUM(m) FROM t WHERE NOT two = 1",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE sparse IN (5, 77, 2999) OR m > 400",
+    "SELECT clustered, COUNT(*), SUM(m) FROM t WHERE NOT clustered IN (0, 3) AND two = 0 GROUP BY clustered",
+])
+def test_bitset_leaves_outside_gates_with_tile_groups(engine, q, plan, monkeypatch):
+    """DocId-bitset leaves that are not gates (negated, OR-ed with a column leaf) read their bitset words per lane
+    in every step of a 4-tile group, padding tiles and steps past the block's range included: segments whose
+    tile counts are not multiples of 4 (1, 5, 7 tiles), fused scan and tile-level select, against the oracle
+    (the bitsets carry slack behind their words for those reads)."""
+    monkeypatch.setenv("PINOT_AMD_INV_POLICY", "always")
+    if plan == "scan":
+        monkeypatch.setenv("PINOT_AMD_SELECT", "never")
+        monkeypatch.setenv("PINOT_AMD_SCAN_GROUP", "4")
+        monkeypatch.setenv("PINOT_AMD_FILTER_GATE", "0")
+    else:
+        monkeypatch.setenv("PINOT_AMD_SELECT", "always")
+        monkeypatch.setenv("PINOT_AMD_SEL_GROUP", "4")
+    bufs = [_container_segment(n, 20 + i) for i, n in enumerate((300, 5000, 7 * 1024 + 3))]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og if nm else {(): og[()]})
