@@ -2333,7 +2333,7 @@ static int run_plan(pinot_amd_result* r) {
           if (!r->trim && r->spill_words > 0)
             HIP_OK(launch_spill_passes(H, r->nw, r->launches[li].grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
                                        (unsigned long long*)r->sp_sorted.p, r->q, (uint64_t*)r->acc.p, r->spill_agg_grid,
-                                       r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "1") ? 1 : 0, st));
+                                       r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "0") ? 0 : 1, st));
         }
       if (r->trim) {
         const int32_t nb = r->batch_nsegs[b];
@@ -3315,9 +3315,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   // of a B-byte column (64 / B docs) is fetched when any of its docs matches: 1 - (1 - s)^(64 / B) of it at
   // selectivity s (the segments' exact match counts). Chosen when the bytes it reads -- the filter columns, then
   // the fetched share of every column read after the filter (a filter column that is also a key or value is
-  // read twice) -- are at most 3/4 of the fused scan's. PINOT_AMD_FILTER_GATE=0|1 pins it.
+  // read twice) -- are at most 3/4 of the fused scan's. Opt-in (PINOT_AMD_FILTER_GATE=auto: this model,
+  // =1: forced): measured on SSB it lost to the 4-tile fused scan and to the select pass on every query but
+  // Q4.1 (1.075 -> 1.038 ms; Q1.1 0.641 -> 0.790, Q3.1 0.852 -> 1.053: profiles/r05/sweep_ssb_fgate.txt) --
+  // these scans run near the HBM rate already, and the gate's one tile per step and a-tile-ahead filter cost
+  // more issue than the skipped sectors save.
   if (!base.select && r->kind == PLAN_DENSE && !base.partitioned && !r->admit && !filter_only && q.nacc > 0 && np > 0 &&
-      !env_is("PINOT_AMD_FILTER_GATE", "0")) {
+      (env_is("PINOT_AMD_FILTER_GATE", "1") || env_is("PINOT_AMD_FILTER_GATE", "auto"))) {
     bool ok = true;  // docId-bitset leaves gate through the inverted-index path instead
     for (size_t k = 0; k < order.size() && ok; ++k)
       for (int si = 0; si < n; ++si) ok &= hsegs[si].leaves[k].kind != LEAF_DOC_BITSET;

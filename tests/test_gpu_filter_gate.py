@@ -95,8 +95,9 @@ def test_gated_ssb_golden(engine, gate, split):
 
 
 def test_planner_choice_on_ssb_segments(engine, monkeypatch):
-    """The planner's own choice (gate or not, select or not) on the SF-scaled generator's segments."""
-    monkeypatch.delenv("PINOT_AMD_FILTER_GATE", raising=False)
+    """The opt-in cost model's choice (PINOT_AMD_FILTER_GATE=auto: gate or not, select or not) on the SF-scaled
+    generator's segments."""
+    monkeypatch.setenv("PINOT_AMD_FILTER_GATE", "auto")
     bufs = [ssb.lineorder_flat_segment(f"fg{i}", 200_003 + i, seed=10 + i) for i in range(2)]
     segs = [engine.ImmutableSegment(b) for b in bufs]
     for name, sql in ssb.SSB_QUERIES:
