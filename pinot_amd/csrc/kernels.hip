@@ -345,6 +345,8 @@ __global__ void hash_merge_kernel(const unsigned long long* skeys, int64_t scap,
 // of per doc -- the map-based holders' group-id lookups (DictionaryBasedGroupKeyGenerator.java:444-900)
 // with their per-doc random accesses moved on-die.
 // ------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;
+
 __device__ __forceinline__ uint64_t key_hash_rt(const uint64_t* kw, int nw) {
   uint64_t x = 0x9E3779B97F4A7C15ull;
   for (int w = 0; w < nw; ++w) x = fmix64(x ^ kw[w]);
@@ -492,10 +494,13 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
       for (int n = 0; n < 64; ++n) {
         bool ok = true;
         for (int w = 0; w < nw && ok; ++w) {
-          unsigned long long* pw = LK + (uint32_t)w * (uint32_t)S + s;
-          unsigned long long c = *(volatile unsigned long long*)pw;
+          // the table word through an LDS pointer: a volatile access through the generic one compiled to a
+          // volatile flat load and a vmcnt(0) wait per probe
+          LdsU64* pw = (LdsU64*)(LK + (uint32_t)w * (uint32_t)S + s);
+          unsigned long long c = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (c == ~0ull) {
-            c = atomicCAS(pw, ~0ull, (unsigned long long)kw[w]);
+            __hip_atomic_compare_exchange_strong(pw, &c, (unsigned long long)kw[w], __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
             if (c == ~0ull) c = kw[w];
           }
           ok = c == kw[w];
@@ -506,20 +511,24 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
         }
         s = s + 1u == (uint32_t)S ? 0u : s + 1u;
       }
-      uint64_t* base;
-      int64_t stride;
-      if (ls >= 0) {
-        base = LA + ls;
-        stride = S;
-      } else {  // no LDS slot: straight into the HBM table
-        const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
-        if (slot < 0) {
-          atomicAdd(H.overflow, 1ull);
-          continue;
+      if (ls >= 0) {  // the LDS slot (the accumulator words addressed from the shared array: LDS atomics)
+        atomicAdd(reinterpret_cast<unsigned long long*>(LA + ls), 1ull);
+        int j = nw;
+        for (int a = 1; a < nacc; ++a) {
+          const int32_t op = q.acc_op[a];
+          if (op == ACC_HI) continue;
+          spill_apply(op, LA + (int64_t)a * S + ls, LA + (int64_t)(a + 1 < nacc ? a + 1 : a) * S + ls, r[j++]);
         }
-        base = acc + slot;
-        stride = H.cap;
+        continue;
       }
+      // no LDS slot: straight into the HBM table
+      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
+      if (slot < 0) {
+        atomicAdd(H.overflow, 1ull);
+        continue;
+      }
+      uint64_t* base = acc + slot;
+      const int64_t stride = H.cap;
       atomicAdd(reinterpret_cast<unsigned long long*>(base), 1ull);
       int j = nw;
       for (int a = 1; a < nacc; ++a) {
@@ -931,10 +940,17 @@ struct RoaringContainer {
   uint64_t offset;   // byte offset of the container payload inside the staged inverted index
 };
 
+// a job's device pointers as global-address-space pointers: loads through the generic ones compiled to flat
+// loads, which also count against lgkmcnt -- every wait for the expansion's LDS atomics then waited for them
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+
 // descriptor of the container at position ci of a job's selection
 __device__ __forceinline__ RoaringContainer expand_desc(const ExpandJob& J, int32_t ci) {
   if (J.psel) {
-    const unsigned long long d = J.psel[ci];
+    const unsigned long long d = gptr(J.psel)[ci];
     RoaringContainer c;
     c.key = (uint32_t)(d >> 50) & 7u;  // the chunk within the item's chunk group
     c.kind = (uint32_t)(d >> 48) & 3u;
@@ -943,7 +959,14 @@ __device__ __forceinline__ RoaringContainer expand_desc(const ExpandJob& J, int3
     c.offset = d & 0xFFFFFFFFull;
     return c;
   }
-  return J.conts[J.sel[ci]];
+  const __attribute__((address_space(1))) RoaringContainer* cp = gptr(J.conts) + gptr(J.sel)[ci];
+  RoaringContainer c;
+  c.key = cp->key;
+  c.kind = cp->kind;
+  c.count = cp->count;
+  c.pad = cp->pad;
+  c.offset = cp->offset;
+  return c;
 }
 
 // Plan time: pack the selected containers' descriptors in sel order (ExpandJob::psel): byte offset |
@@ -974,7 +997,7 @@ constexpr int kExpandPer = 4;  // containers per lane per round: their loads are
 template <int G, int kPer = kExpandPer>
 __device__ __forceinline__ void expand_item(const ExpandJob& J, int32_t k, uint32_t* lbits, int32_t* bigq, int32_t* nbig) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int32_t g0 = J.grp[k], g1 = J.grp[k + 1];
+  const int32_t g0 = gptr(J.grp)[k], g1 = gptr(J.grp)[k + 1];
   for (int32_t base = g0; base < g1; base += kBlock * kPer) {
     // every load of the round first (selected index, descriptor, small-array payload), then the LDS work
     int32_t si[kPer];  // position in the job's sel order, -1: none
@@ -996,7 +1019,7 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, int32_t k, uint3
       if (small) {
         // only the 16-byte pieces the entries reach (halfwords odd .. odd + count - 1): with a few docs per
         // container (selective IN lists) one piece, so the neighbouring containers' pieces share lines
-        const u32x4a4* p4 = reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull));
+        const __attribute__((address_space(1))) u32x4a4* p4 = gptr(reinterpret_cast<const u32x4a4*>(J.inv + (c[u].offset & ~3ull)));
         const uint32_t reach = odd + c[u].count;
         const u32x4a4 a = p4[0];
         u32x4a4 b = (u32x4a4)(0u), d = (u32x4a4)(0u);
@@ -1030,25 +1053,25 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, int32_t k, uint3
     const int nb = *nbig;
     for (int qi = wave; qi < nb; qi += kBlock / 64) {
       const RoaringContainer c = expand_desc(J, bigq[qi]);
-      const uint8_t* p = J.inv + c.offset;
+      const __attribute__((address_space(1))) uint8_t* p = gptr(J.inv) + c.offset;
       uint32_t* lb = lbits + 2048 * (G == 1 ? 0u : c.key % (uint32_t)G);
       if (c.kind == 1) {
         for (int i = lane; i < 1024; i += 64) {
-          const uint64_t w = *reinterpret_cast<const uint64_t*>(p + 8 * i);  // LE
+          const uint64_t w = *reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(p + 8 * i);  // LE
           if (w) {
             atomicOr(&lb[2 * i], (uint32_t)w);
             atomicOr(&lb[2 * i + 1], (uint32_t)(w >> 32));
           }
         }
       } else if (c.kind == 0) {
-        const uint16_t* p16 = reinterpret_cast<const uint16_t*>(p);
+        const __attribute__((address_space(1))) uint16_t* p16 = reinterpret_cast<const __attribute__((address_space(1))) uint16_t*>(p);
         for (uint32_t e = lane; e < c.count; e += 64) {
           const uint32_t d = p16[e];
           atomicOr(&lb[d >> 5], 1u << (d & 31));
         }
       } else {
         for (uint32_t r = 0; r < c.count; ++r) {
-          const uint8_t* q = p + 2 + 4 * r;
+          const __attribute__((address_space(1))) uint8_t* q = p + 2 + 4 * r;
           const uint32_t s0 = q[0] | (q[1] << 8);
           const uint32_t e0 = s0 + (q[2] | (q[3] << 8));  // inclusive, < 65536
           const uint32_t w0 = s0 >> 5, w1 = e0 >> 5;
@@ -1090,7 +1113,9 @@ __global__ void __launch_bounds__(kBlock) roaring_expand_chunks_kernel(const Exp
     const int64_t w_begin = (int64_t)k * 1024 * G;
     for (int i = tid; i < 1024 * G; i += kBlock) {
       const int64_t w = w_begin + i;
-      if (w < J.nwords) J.bitset[w] = (unsigned long long)lbits[2 * i] | ((unsigned long long)lbits[2 * i + 1] << 32);
+      if (w < J.nwords)
+        ((__attribute__((address_space(1))) unsigned long long*)J.bitset)[w] =
+            (unsigned long long)lbits[2 * i] | ((unsigned long long)lbits[2 * i + 1] << 32);
     }
     __syncthreads();
   }
