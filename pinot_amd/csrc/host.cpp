@@ -3412,6 +3412,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (S * slot_bytes <= lds_max - reserve) {
       base.hash_lds = (int)S;
       base.hash_spill = spill;
+      base.hash_admit = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_i64("PINOT_AMD_HASH_LDS_ADMIT", 0)));
       base.scan_nsub = kPartSub;
       hash_lds_bytes = S * slot_bytes;
     } else {

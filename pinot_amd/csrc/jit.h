@@ -162,6 +162,9 @@ struct JitPlan {
   // that tile load only for lanes with a matching doc -- at a few percent selectivity most 64-byte sectors of
   // the wide value columns are never fetched (late materialisation inside the scan, no selection vector)
   bool filter_gate = false;
+  // hash plans' LDS first level: a doc may insert its key into an EMPTY slot with probability 2^-hash_admit
+  // (0: always) -- admission by recurrence, so the slots hold a skewed distribution's head
+  int hash_admit = 0;
   // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
   // results; isolates the lookup's traffic in A/B profiles)
   bool diag_admit_off = false;
