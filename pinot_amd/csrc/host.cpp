@@ -1395,6 +1395,7 @@ struct pinot_amd_result {
   // second level of the LDS-privatised hash plan (JitPlan::hash_spill, DevHash::spill)
   DevBuf sp_rec, sp_sorted, sp_cnt, sp_hist, sp_offs, sp_pbeg;
   int64_t spill_cap = 0, spill_grid = 0;
+  int64_t spill_cap_max = 0;  // regions' ceiling: the scan blocks' docs, within PINOT_AMD_SPILL_MAX_BYTES
   int spill_words = 0, spill_slots = 0, spill_agg_grid = 1;
   bool cap_known = false, ovf_pending = false;
   bool trim = false;                   // numGroupsLimit trimming (scan tables keyed by (key, segment))
@@ -2260,6 +2261,25 @@ static int64_t known_hash_capacity(const std::string& key) {
   return it == g_cap_cache.end() ? 0 : it->second;
 }
 
+// Spill-region capacities (records per scan block) an execution of a query shape over a segment set needed
+// (pinot_amd_result::cap_key): a region that overflowed sends its further records to the HBM table one doc at a
+// time (correct, slow: the wide-key bench at 100 segments ran 28.2 ms instead of 22.1 with room for them), so
+// a re-issued query allocates the regions the last execution needed.
+static std::unordered_map<std::string, int64_t> g_spill_cache;  // guarded by g_cap_mu
+
+static void remember_spill_capacity(const std::string& key, int64_t recs) {
+  if (key.empty()) return;
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  if (g_spill_cache.size() >= 4096) g_spill_cache.clear();
+  int64_t& c = g_spill_cache[key];
+  c = std::max(c, recs);
+}
+static int64_t known_spill_capacity(const std::string& key) {
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  auto it = g_spill_cache.find(key);
+  return it == g_spill_cache.end() ? 0 : it->second;
+}
+
 // grow an untrimmed hash plan's table 4x, at most to its ceiling (*grown false: already there)
 static int grow_hash(pinot_amd_result* r, bool* grown) {
   *grown = false;
@@ -2281,6 +2301,19 @@ static int run_plan(pinot_amd_result* r) {
   r->ovf_pending = false;
   hipStream_t st = r->stream;
   r->compacted = false;
+  if (r->spill_words > 0 && !r->cap_key.empty()) {
+    // an execution of this shape overflowed its spill regions since they were sized: larger regions (the old
+    // ones are freed first: hipFree waits for the work still reading them)
+    const int64_t want = std::min(known_spill_capacity(r->cap_key), r->spill_cap_max);
+    if (want > r->spill_cap) {
+      const size_t bytes = (size_t)r->spill_grid * (size_t)want * (size_t)r->spill_words * 8;
+      r->sp_rec.reset();
+      r->sp_sorted.reset();
+      if (int rc = r->sp_rec.alloc(bytes)) return rc;
+      if (int rc = r->sp_sorted.alloc(bytes)) return rc;
+      r->spill_cap = want;
+    }
+  }
   HIP_OK(hipEventRecord(r->ev0, st));
   // inverted-index leaves: expand roaring containers into dense doc bitsets
   bool all_fused = !r->launches.empty();
@@ -3412,7 +3445,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (S * slot_bytes <= lds_max - reserve) {
       base.hash_lds = (int)S;
       base.hash_spill = spill;
-      base.hash_admit = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_i64("PINOT_AMD_HASH_LDS_ADMIT", 0)));
+      // admission by recurrence (a doc inserts its key with probability 2^-5): the wide-key bench at 100 segments
+      // 22.1 -> 15.4 ms, the LDS slots then holding the Zipf head instead of the first keys seen
+      // (profiles/r05/sweep_wk_cap.txt); PINOT_AMD_HASH_LDS_ADMIT=n sets 2^-n, 0 inserts every key
+      base.hash_admit = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_i64("PINOT_AMD_HASH_LDS_ADMIT", 5)));
       base.scan_nsub = kPartSub;
       hash_lds_bytes = S * slot_bytes;
     } else {
@@ -3998,6 +4034,13 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const double budget = (double)env_i64("PINOT_AMD_SPILL_BYTES", (int64_t)8 << 30);
       r->spill_cap = std::max<int64_t>(64, std::min<int64_t>(per_max * kTileDocs,
                                                               (int64_t)(budget / ((double)gmax * r->spill_words * 8.0))));
+      // an earlier execution of this query shape over these segments needed more (its regions overflowed): up to
+      // PINOT_AMD_SPILL_MAX_BYTES (default 32 GiB per copy); run_plan grows them the same way later
+      const double maxb = (double)env_i64("PINOT_AMD_SPILL_MAX_BYTES", (int64_t)32 << 30);
+      r->spill_cap_max = std::max<int64_t>(64, std::min<int64_t>(per_max * kTileDocs,
+                                                                  (int64_t)(maxb / ((double)gmax * r->spill_words * 8.0))));
+      if (const int64_t known = known_spill_capacity(r->cap_key))
+        r->spill_cap = std::max(r->spill_cap, std::min(known, r->spill_cap_max));
       r->spill_grid = gmax;
       if (int rc = r->sp_rec.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
       if (int rc = r->sp_sorted.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
@@ -4258,6 +4301,14 @@ static int check_overflow(pinot_amd_result* r) {
   if (c[3 * r->launches.size() + 1] != 0)
     return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
                 (long long)c[3 * r->launches.size() + 1]);
+  if (r->spill_words > 0 && r->spill_grid > 0 && !r->cap_key.empty()) {
+    // the last launch's per-block record counts: a region that ran out sizes the next execution's regions
+    std::vector<uint32_t> cnt((size_t)r->spill_grid);
+    HIP_OK(hipMemcpyAsync(cnt.data(), r->sp_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const int64_t mx = (int64_t)*std::max_element(cnt.begin(), cnt.end());
+    if (mx > r->spill_cap) remember_spill_capacity(r->cap_key, mx + mx / 8);
+  }
   if (r->sel_ctr.n) {
     std::vector<unsigned long long> sc(r->sel_ctr.n / 8);
     HIP_OK(hipMemcpyAsync(sc.data(), r->sel_ctr.p, r->sel_ctr.n, hipMemcpyDeviceToHost, st));

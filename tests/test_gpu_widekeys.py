@@ -27,8 +27,12 @@ def wide():
 
 @pytest.mark.parametrize("env", [{}, {"PINOT_AMD_HASH_LDS_SLOTS": "64"}, {"PINOT_AMD_HASH_LDS": "0"},
                                  {"PINOT_AMD_HASH_INIT_SLOTS": "64"},
-                                 {"PINOT_AMD_HASH_INIT_SLOTS": "64", "PINOT_AMD_HASH_LDS_SLOTS": "128"}],
-                         ids=["lds", "lds64", "nolds", "grow", "grow-lds128"])
+                                 {"PINOT_AMD_HASH_INIT_SLOTS": "64", "PINOT_AMD_HASH_LDS_SLOTS": "128"},
+                                 {"PINOT_AMD_HASH_LDS_ADMIT": "0"}, {"PINOT_AMD_HASH_LDS_ADMIT": "8"},
+                                 {"PINOT_AMD_SPILL_BYTES": "4096"}, {"PINOT_AMD_HASH_SPILL": "0"},
+                                 {"PINOT_AMD_SPILL_SORT": "0"}],
+                         ids=["lds", "lds64", "nolds", "grow", "grow-lds128", "admit-all", "admit-1in256",
+                              "spill-overflow", "nospill", "spill-unsorted"])
 def test_widekeys_hash_plan_vs_oracle(wide, env, monkeypatch):
     E, bufs, segs, exp = wide
     monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")  # every case sizes (and grows) its own table
@@ -40,7 +44,7 @@ def test_widekeys_hash_plan_vs_oracle(wide, env, monkeypatch):
     assert len(got) == len(exp) > 10_000
     assert got == exp
     assert sum(v[0] for v in got.values()) == res.num_docs_matched()
-    res.execute_again()  # a re-execution (the grown table is kept) gives the same groups
+    res.execute_again()  # a re-execution (the grown table / spill regions are kept) gives the same groups
     assert res.groups() == exp
 
 
@@ -97,3 +101,18 @@ def test_hash_growth_lands_on_the_ceiling(monkeypatch):
     got = res.groups()
     assert len(got) == len(exp) > 3000 and got == exp
     assert res.plan_timing()["hash_slots"] == 8192
+
+
+def test_spill_regions_grow_after_an_overflow(wide, monkeypatch):
+    """Spill regions far too small (64 records per scan block): the records past them take the HBM table, the
+    groups are exact; the fetch remembers what the blocks needed, so the next execution of the same result and a
+    re-issued query run with regions that hold every record -- same groups."""
+    E, bufs, segs, exp = wide
+    monkeypatch.setenv("PINOT_AMD_SPILL_BYTES", "4096")
+    monkeypatch.setenv("PINOT_AMD_HASH_LDS_ADMIT", "8")  # most keys miss the LDS level
+    r1 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    assert r1.groups() == exp
+    r1.execute_again()
+    assert r1.groups() == exp
+    r2 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    assert r2.groups() == exp
