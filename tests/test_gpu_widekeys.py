@@ -92,6 +92,8 @@ def test_hash_growth_lands_on_the_ceiling(monkeypatch):
     monkeypatch.setenv("PINOT_AMD_HASH_INIT_SLOTS", "64")
     monkeypatch.setenv("PINOT_AMD_HASH_MAX_PROBE", "64")
     monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    # every key into the LDS level as it comes (the insertion order into the HBM table this case was sized for)
+    monkeypatch.setenv("PINOT_AMD_HASH_LDS_ADMIT", "0")
     rng = np.random.default_rng(3)
     bufs = [random_segment(rng, 4_000, name="hg0", bits_cards=(300, 37))]
     segs = [E.ImmutableSegment(b) for b in bufs]
