@@ -53,7 +53,8 @@ def main(src, dst, only=None):
             durs[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
         plan = {k: v for k, v in durs.items() if len(v) >= execs_trace - 1 and
                 any(s in k for s in ("pinot", "roaring", "partition", "exclusive", "init_acc", "trim", "hash", "admit",
-                                     "allot", "merge", "pack_sel", "gather", "presence", "bitset", "lhash"))}
+                                     "allot", "merge", "pack_sel", "gather", "presence", "bitset", "lhash", "spill",
+                                     "seg_cut", "sext_hi"))}
         # A kernel with more dispatches than executions also ran the planner's filter-only match-count
         # probe (selection-vector cost model, numGroupsLimit bound): once in the cold execution since the
         # round-3 probe cache (dispatch 0), twice before it (dispatches 0 and 2). Plan-time work, dropped.
