@@ -3736,6 +3736,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
       jp.flush_every = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_EVERY", 1)));
       jp.flush_par = !env_is("PINOT_AMD_FLUSH_PAR", "0");
+      jp.flush_group = env_is("PINOT_AMD_FLUSH_GROUP", "1");
       jp.scatter_batch = !env_is("PINOT_AMD_SCATTER_BATCH", "0");
     }
     {  // algorithmic bytes: each decoded column once (fixed-bit at its width, raw at its value width)

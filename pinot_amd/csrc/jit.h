@@ -108,6 +108,9 @@ struct JitPlan {
   // one 16 / 8 B unit, owners found by a binary search over the lanes' prefix sums) instead of one run
   // after another with the whole wave on each run
   bool flush_par = true;
+  // 16-byte records: the flush copies four ready partitions per wave step, a 16-lane group each (consecutive
+  // lanes store consecutive records), instead of the lane-parallel flush's per-unit owner search
+  bool flush_group = false;
   // partitioned plans: 256-thread groups per count / scatter block (4: one CU-wide block per CU with all the
   // LDS for staging; 2 / 1: two / four blocks per CU, each with that share of the LDS)
   int part_sub = kPartSub;

@@ -196,3 +196,27 @@ def test_highcard_select_into_hbm_table(engine, monkeypatch, where):
     res.execute_again()
     assert res.num_docs_matched() == nm
     assert_same_groups(res.groups(), og)
+
+
+@pytest.mark.parametrize("env", [{"PINOT_AMD_FLUSH_GROUP": "1"}, {"PINOT_AMD_FLUSH_GROUP": "1", "PINOT_AMD_STAGE_CAP": "6"},
+                                 {"PINOT_AMD_FLUSH_GROUP": "1", "PINOT_AMD_SAMPLE_STRIDE": "8"},
+                                 {"PINOT_AMD_FLUSH_GROUP": "1", "PINOT_AMD_FLUSH_EVERY": "3"},
+                                 {"PINOT_AMD_FLUSH_GROUP": "0"}],
+                         ids=["group", "group-cap6", "group-sampled", "group-every3", "lane-parallel"])
+def test_highcard_flush_variants(engine, monkeypatch, env):
+    """configs[3]'s query and data (16-byte records) through the scatter's flush variants -- four ready
+    partitions per wave step in 16-lane groups (exact counts at this size, sampled allotments with the overflow
+    slab at stride 8, tiny staging, a slower flush cadence) and the lane-parallel flush -- against the oracle."""
+    from pinot_amd import datagen
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    bufs = [datagen.highcard_segment(f"hf{i}", 700_001 + 13 * i, seed=300 + i) for i in range(2)]
+    segs = [engine.ImmutableSegment(b) for b in bufs]
+    q = datagen.HIGHCARD_QUERY
+    res = engine.ServerQueryExecutor().execute(q, segs)
+    assert res.kernel_info() == "jit-partitioned", res.kernel_info()
+    nm, og = oracle.execute(q, bufs)
+    assert res.num_docs_matched() == nm
+    assert_same_groups(res.groups(), og)
+    res.execute_again()
+    assert_same_groups(res.groups(), og)
