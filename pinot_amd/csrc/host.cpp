@@ -23,6 +23,7 @@
 #include <new>
 #include <stdexcept>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -1779,15 +1780,21 @@ constexpr size_t kLeafCacheMax = 256;  // entries per segment (cleared when full
 
 // make_leaf_uncached through the segment's leaf cache. The key is everything the resolution reads: the
 // predicate, the slot, whether its column is decoded anyway, and the knobs of the inverted-index policy.
+static std::string leaf_cache_key(const PredSpec& p, int slot, bool decoded_anyway) {
+  const char* pol = getenv("PINOT_AMD_INV_POLICY");
+  return preds_signature({p}) + "|" + std::to_string(slot) + "|" + (decoded_anyway ? "1" : "0") + "|" +
+         std::to_string(expand_group()) + "|" + (pol ? pol : "");
+}
+
+// key: leaf_cache_key(p, slot, decoded_anyway) when the caller built it once for every segment
 static int make_leaf_for_segment(pinot_amd_result* r, int si, pinot_amd_segment* seg, const PredSpec& p,
                                  const Column& c, int slot, DevLeaf* L, bool* needs_slot, hipStream_t st,
-                                 bool decoded_anyway) {
-  const bool use_cache = !env_is("PINOT_AMD_LEAF_CACHE", "0");
-  std::string key;
+                                 bool decoded_anyway, const std::string* key_in = nullptr) {
+  const bool use_cache = key_in != nullptr || !env_is("PINOT_AMD_LEAF_CACHE", "0");
+  std::string key_own;
+  const std::string& key = key_in ? *key_in : key_own;
   if (use_cache) {
-    const char* pol = getenv("PINOT_AMD_INV_POLICY");
-    key = preds_signature({p}) + "|" + std::to_string(slot) + "|" + (decoded_anyway ? "1" : "0") + "|" +
-          std::to_string(expand_group()) + "|" + (pol ? pol : "");
+    if (!key_in) key_own = leaf_cache_key(p, slot, decoded_anyway);
     std::shared_ptr<const LeafCacheEntry> e;
     {
       std::lock_guard<std::mutex> g(g_leaf_mu);
@@ -2474,6 +2481,28 @@ extern "C" {
 
 // wall-clock milliseconds of the planning phases of one execute (diagnostics: where a cold / cached
 // query's host time goes)
+// hipModuleOccupancyMaxActiveBlocksPerMultiprocessor per (kernel, block size, dynamic LDS), memoised: the planner
+// asks for every launch of every execution, and a kernel's occupancy never changes
+static hipError_t occupancy_blocks(int* out, hipFunction_t fn, int threads, size_t shmem) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t>, int> memo;
+  const auto key = std::make_tuple((const void*)fn, threads, shmem);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) {
+      *out = it->second;
+      return hipSuccess;
+    }
+  }
+  const hipError_t e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(out, fn, threads, shmem);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(mu);
+    memo[key] = *out;
+  }
+  return e;
+}
+
 struct PlanClock {
   std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
   std::string* out;
@@ -2561,15 +2590,25 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   std::vector<std::vector<int>> leaf_slot_col(n, std::vector<int>(np, -1));
   int nclauses = 0;
   for (size_t pi = 0; pi < np; ++pi) nclauses = std::max(nclauses, Q.preds[pi].clause + 1);
+  // per predicate, once: whether its column is decoded anyway, and its leaf-cache key (the same on every segment)
+  std::vector<char> pred_decoded(np, 0);
+  std::vector<std::string> pred_key(np);
+  for (size_t pi = 0; pi < np; ++pi) {
+    const PredSpec& p = Q.preds[pi];
+    bool d = std::find(Q.group_by.begin(), Q.group_by.end(), p.column) != Q.group_by.end();
+    for (auto& a : Q.aggs) d |= a.column == p.column || a.column2 == p.column;
+    pred_decoded[pi] = d ? 1 : 0;
+    pred_key[pi] = leaf_cache_key(p, -1, d);
+  }
+  const bool leaf_cache = !env_is("PINOT_AMD_LEAF_CACHE", "0");
   for (int si = 0; si < n; ++si) {
     for (size_t pi = 0; pi < np; ++pi) {
       const PredSpec& p = Q.preds[pi];
       const Column& c = *segs[si]->cols.at(p.column);
       bool needs_slot = false;
-      bool decoded_anyway = std::find(Q.group_by.begin(), Q.group_by.end(), p.column) != Q.group_by.end();
-      for (auto& a : Q.aggs) decoded_anyway |= a.column == p.column || a.column2 == p.column;
+      const bool decoded_anyway = pred_decoded[pi] != 0;
       int rc = make_leaf_for_segment(r, si, segs[si], p, c, -1, &seg_leaves[si][pi], &needs_slot, r->stream,
-                                     decoded_anyway);
+                                     decoded_anyway, leaf_cache ? &pred_key[pi] : nullptr);
       if (rc) return rc;
       if (needs_slot) leaf_slot_col[si][pi] = slot_of(p.column);
     }
@@ -3806,7 +3845,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.fd_q = L.q;
       L.fd_q.total_tiles = ftiles;
       int nf = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nf, L.jit_fd->fn, kBlock, 0) != hipSuccess || nf < 1) nf = 1;
+      if (occupancy_blocks(&nf, L.jit_fd->fn, kBlock, 0) != hipSuccess || nf < 1) nf = 1;
       L.fd_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, ftiles));
       L.fd_full_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nf, tiles));
     }
@@ -3827,7 +3866,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.jit_sp = jit_get(js, &r->jit_status);
       if (!L.jit_sp) return fail(PINOT_AMD_EUNSUPPORTED, "presence kernel unavailable: %s", r->jit_status.c_str());
       int ns = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, L.jit_sp->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
+      if (occupancy_blocks(&ns, L.jit_sp->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
       L.sp_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, tiles));
     }
     L.scan_nsub = jp.partitioned ? 1 : jp.scan_nsub;
@@ -3891,22 +3930,22 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
       int nb = 0;
       L.part_sub = jp.part_sub;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn_scatter, kBlock * jp.part_sub, L.shmem_scatter) !=
+      if (occupancy_blocks(&nb, L.jit->fn_scatter, kBlock * jp.part_sub, L.shmem_scatter) !=
               hipSuccess || nb < 1)
         nb = 1;
       per_cu = nb;
       int na = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&na, L.jit->fn_agg, 1024, L.shmem_agg) != hipSuccess || na < 1)
+      if (occupancy_blocks(&na, L.jit->fn_agg, 1024, L.shmem_agg) != hipSuccess || na < 1)
         na = 1;
       L.agg_grid = cus * na;
       if (L.jit_atomic) {
         int nt = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nt, L.jit_atomic->fn, kBlock, 0) != hipSuccess || nt < 1) nt = 1;
+        if (occupancy_blocks(&nt, L.jit_atomic->fn, kBlock, 0) != hipSuccess || nt < 1) nt = 1;
         L.atomic_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * nt, tiles));
       }
       if (L.jit_sample) {
         int ns = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ns, L.jit_sample->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
+        if (occupancy_blocks(&ns, L.jit_sample->fn, kBlock, 0) != hipSuccess || ns < 1) ns = 1;
         const int64_t vt = (tiles + L.part.sample_stride - 1) / L.part.sample_stride;
         L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
       }
@@ -3918,8 +3957,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.scan_nsub = 1;
       L.gather_threads = jp.lds ? kBlock * jp.scan_nsub : kBlock;
       int nb = 0, ng = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
+      if (occupancy_blocks(&nb, L.jit->fn, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+      if (occupancy_blocks(&ng, L.jit->fn_gather, L.gather_threads, L.shmem) != hipSuccess ||
           ng < 1)
         ng = 1;
       // select blocks per CU: fewer, longer-running waves reserve vector chunks on the shared counter
@@ -3958,7 +3997,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       max_sel = std::max<int64_t>(max_sel, chunks * chunk + 64);
     } else {
       int nb = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||
+      if (occupancy_blocks(&nb, L.jit->fn, kBlock * L.scan_nsub, L.shmem) != hipSuccess ||
           nb < 1)
         nb = 1;
       per_cu = nb;
