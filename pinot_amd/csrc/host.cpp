@@ -2066,6 +2066,66 @@ static int cached_remap(const pinot_amd_segment* s, const std::string& col, cons
 // ------------------------------------------------------------------------------------------------
 // execution
 // ------------------------------------------------------------------------------------------------
+// Diagnostics (PINOT_AMD_DIAG_SCATTER=1): FNV checksum of the forward-index bytes and the remaps of a launch's
+// segments (synchronises the stream): a plan must never change them
+static uint64_t diag_segment_sum(const Launch& L, hipStream_t st) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  std::vector<DevSegment> ds(L.segs.size());
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(ds.data(), L.d_segs.p, ds.size() * sizeof(DevSegment), hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  std::vector<uint8_t> buf;
+  for (const DevSegment& d : ds)
+    for (int c = 0; c < kMaxSlots; ++c) {
+      const DevColumn& col = d.cols[c];
+      if (!col.data) continue;
+      const size_t n = col.enc == ENC_FIXED_BIT ? (size_t)((d.num_docs * col.bits + 7) / 8)
+                       : col.enc == ENC_RAW ? (size_t)d.num_docs * (col.type == T_INT || col.type == T_FLOAT ? 4 : 8) : 0;
+      buf.resize(n);
+      if (n && hipMemcpy(buf.data(), col.data, n, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+      for (uint8_t b : buf) h = (h ^ b) * 0x100000001b3ull;
+      if (col.remap && col.card > 0) {
+        buf.resize((size_t)col.card * 4);
+        if (hipMemcpy(buf.data(), col.remap, buf.size(), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        for (uint8_t b : buf) h = (h ^ b) * 0x100000001b3ull;
+      }
+    }
+  return h;
+}
+
+// Diagnostics of an exact partitioned launch (PINOT_AMD_DIAG_SCATTER=1; the record buffer was filled with 0xFF
+// before the scatter): the records the scatter left unwritten, by partition and scatter block, to stderr.
+static void diag_scatter_report(const Launch& L, unsigned count_grid, hipStream_t st) {
+  const int P = L.part.nparts, R = L.rec_bytes, grid = L.grid;
+  std::vector<int64_t> pb((size_t)P + 1), offs((size_t)P * count_grid);
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(pb.data(), L.part.part_begin, pb.size() * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(offs.data(), L.part.offs, offs.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  const int64_t total = pb[P];
+  std::vector<uint8_t> rec((size_t)std::max<int64_t>(total, 0) * R);
+  if (total > 0 && hipMemcpy(rec.data(), L.part.rec, rec.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+  int64_t unwritten = 0;
+  std::string ex;
+  for (int64_t i = 0; i < total; ++i) {
+    bool sentinel = true;
+    for (int b = 0; b < R && sentinel; ++b) sentinel = rec[(size_t)i * R + b] == 0xFF;
+    if (!sentinel) continue;
+    ++unwritten;
+    if (unwritten > 12) continue;
+    const int p = (int)(std::upper_bound(pb.begin(), pb.end(), i) - pb.begin()) - 1;
+    int64_t blk = 0;  // the scatter block whose run of partition p holds record i
+    for (int b = 0; b < grid; ++b)
+      if (pb[p] + offs[(size_t)p * count_grid + (size_t)b * kPartCountRatio] <= i) blk = b;
+    const int64_t run0 = pb[p] + offs[(size_t)p * count_grid + (size_t)blk * kPartCountRatio];
+    const int64_t run1 = blk + 1 < grid ? pb[p] + offs[(size_t)p * count_grid + (size_t)(blk + 1) * kPartCountRatio] : pb[p + 1];
+    ex += " [rec " + std::to_string(i) + " part " + std::to_string(p) + " block " + std::to_string(blk) + " run " +
+          std::to_string(run0) + ".." + std::to_string(run1) + " at " + std::to_string(i - run0) + "]";
+  }
+  fprintf(stderr, "DIAG_SCATTER records %lld unwritten %lld grid %d count_grid %u parts %d%s\n", (long long)total,
+          (long long)unwritten, grid, count_grid, P, ex.c_str());
+}
+
 static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table, const DevHash& H) {
   hipStream_t st = r->stream;
   const DevSegment* segs = (const DevSegment*)L.d_segs.p;
@@ -2142,11 +2202,22 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   HIP_OK(launch_partition_offsets(L.part.hist, L.part.nparts, count_grid, L.part.offs, L.part.part_begin, st));
   if (L.jit_atomic)
     HIP_OK(hipModuleLaunchKernel(L.jit_atomic->fn, (unsigned)L.atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
+  // diagnostics (PINOT_AMD_DIAG_SCATTER=1): records the scatter leaves unwritten (a sentinel fill before it)
+  static const bool diag_scatter = env_is("PINOT_AMD_DIAG_SCATTER", "1");
+  const size_t rec_fill = (size_t)L.docs * (size_t)L.rec_bytes;
+  if (diag_scatter) HIP_OK(hipMemsetAsync(L.part.rec, 0xFF, rec_fill, st));
+  const uint64_t diag_sum0 = diag_scatter ? diag_segment_sum(L, st) : 0;  // (before the scatter: after count + offsets)
   HIP_OK(hipModuleLaunchKernel(L.jit->fn_scatter, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem_scatter, st, args,
                                nullptr));
   void* agg_args[] = {(void*)&L.part, (void*)&table};
   HIP_OK(hipModuleLaunchKernel(L.jit->fn_agg, (unsigned)L.agg_grid, 1, 1, 1024, 1, 1, (unsigned)L.shmem_agg, st,
                                agg_args, nullptr));
+  if (diag_scatter) {  // (after the aggregation: the same kernel sequence)
+    diag_scatter_report(L, count_grid, st);
+    const uint64_t s2 = diag_segment_sum(L, st);
+    if (s2 != diag_sum0) fprintf(stderr, "DIAG_SEGSUM changed during the plan: %016llx -> %016llx\n",
+                                 (unsigned long long)diag_sum0, (unsigned long long)s2);
+  }
   return 0;
 }
 

@@ -278,6 +278,8 @@ def test_int_sums_narrow_lds_partials(engine, monkeypatch, narrow):
             assert res.kernel_info().startswith("jit-partitioned"), res.kernel_info()
         _, og = oracle.execute(q, bufs)
         got = res.groups()
-        assert set(got) == set(og)
+        miss, extra = sorted(set(og) - set(got)), sorted(set(got) - set(og))
+        assert not miss and not extra, (res.kernel_info(), len(got), len(og), miss[:8], extra[:8],
+                                        {k: v for k, v in res.plan_timing().items() if not isinstance(v, dict)})
         for k in og:
             assert got[k] == og[k], (q, k, got[k], og[k])
