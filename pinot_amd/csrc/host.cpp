@@ -196,7 +196,10 @@ struct DevBuf {
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
+  bool never_free = false;  // diagnostics (PINOT_AMD_DIAG_FRESH_UPLOADS): an upload's address is never reused
   void release() {
+    if (p && never_free) p = nullptr;
+    never_free = false;
     if (p && !(g_release_to_pool && bsz && dev_pool().put(p, bsz))) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -220,7 +223,18 @@ struct DevBuf {
   // allocate n bytes + pad (zeroed), copy `src` (len bytes) to the front
   int alloc_copy(const void* src, size_t len, size_t pad) {
     release();
-    if (int rc = raw_alloc(len + pad)) return rc;
+    static const bool fresh = getenv("PINOT_AMD_DIAG_FRESH_UPLOADS") && atoi(getenv("PINOT_AMD_DIAG_FRESH_UPLOADS")) == 1;
+    if (fresh && len + pad <= ((size_t)1 << 20)) {
+      n = len + pad;
+      bsz = 0;
+      if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
+        p = nullptr;
+        return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
+      }
+      never_free = true;
+    } else if (int rc = raw_alloc(len + pad)) {
+      return rc;
+    }
     if (!pad) {
       if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
       else HIP_OK(hipMemset(p, 0, n));
