@@ -107,6 +107,9 @@ struct DevPartition {
   uint8_t* ovf_rec;          // overflow slab: records, their partitions, and the count
   uint32_t* ovf_part;
   unsigned long long* ovf_n;
+  // exact plans: incremented by every scatter block whose records in some partition end anywhere but where the
+  // count pass said they would (the host then runs the plan again)
+  unsigned long long* check;
 };
 
 // Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the

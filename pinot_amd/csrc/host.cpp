@@ -3732,7 +3732,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (int rc = r->d_sext.alloc_copy(arrs.data(), arrs.size() * 4, 0)) return rc;
   }
   const size_t nl = r->launches.size();
-  if (int rc = r->matched.alloc((3 * nl + 2) * sizeof(unsigned long long))) return rc;
+  if (int rc = r->matched.alloc((3 * nl + 3) * sizeof(unsigned long long))) return rc;
   HIP_OK(hipMemset(r->matched.p, 0, r->matched.n));
   size_t max_count_cells = 0, max_rec = 0, max_slab = 0, max_slab_docs = 0;
   int64_t max_sel = 0;  // selection-vector entries of the largest select launch
@@ -4099,6 +4099,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
       }
       L.part.counts = (unsigned long long*)r->matched.p + 3 * li;
+      L.part.check = (unsigned long long*)r->matched.p + 3 * nl + 2;
     } else if (jp.select) {
       // select pass: plain 256-thread blocks without LDS; gather pass: the table's block size and LDS
       L.select = true;
@@ -4394,10 +4395,26 @@ static int read_counters(pinot_amd_result* r, std::vector<unsigned long long>* c
   return 0;
 }
 
+// A partitioned execution whose scatter disagreed with its count pass (some block's records short of or past its
+// counted runs -- measured as a transient misread of one block's tiles on the round-5 boxes) is run
+// again, up to three times; *c is re-read after each run.
+static int settle_partitioned(pinot_amd_result* r, std::vector<unsigned long long>* c) {
+  for (int retry = 0; r->kind == PLAN_PARTITIONED && (*c)[3 * r->launches.size() + 2] != 0; ++retry) {
+    if (retry == 3)
+      return fail(PINOT_AMD_EINVAL, "partitioned scatter disagreed with its count pass in %d executions", retry + 1);
+    fprintf(stderr, "pinot_amd: partitioned scatter disagreed with its count pass (%llu partition runs); "
+            "running the plan again\n", (unsigned long long)(*c)[3 * r->launches.size() + 2]);
+    if (int rc = run_plan(r)) return rc;
+    if (int rc = read_counters(r, c)) return rc;
+  }
+  return 0;
+}
+
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_docs_matched: bad arguments");
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
+  if (int rc = settle_partitioned(r, &c)) return rc;
   // per launch: the scan / count pass and the direct-atomic scan both count every matching doc;
   // whichever ran has the total (partitioned plans run one of them)
   int64_t total = 0;
@@ -4487,6 +4504,7 @@ static int check_overflow(pinot_amd_result* r) {
       }
     }
   }
+  if (int rc = settle_partitioned(r, &c)) return rc;
   if (c[3 * r->launches.size() + 1] != 0)
     return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
                 (long long)c[3 * r->launches.size() + 1]);
