@@ -185,63 +185,8 @@ static DevPool& dev_pool() {
   static DevPool* pool = new DevPool();  // never destroyed: blocks outlive static destruction order
   return *pool;
 }
-// Small uploads (descriptors, leaves, remaps: <= 1 MiB) bump-allocated from a per-device ring of 64 x 4 MiB chunks:
-// an address comes back only after the ring went round (a chunk is skipped while any of its uploads is alive), so a
-// plan's descriptors never sit where another plan's descriptors were moments before (PINOT_AMD_UPLOAD_ARENA=1).
-struct UploadArena {
-  static constexpr size_t kChunk = (size_t)4 << 20;
-  static constexpr int kChunks = 64;
-  std::mutex mu;
-  struct Dev { uint8_t* base = nullptr; int cur = 0; size_t off = 0; int live[kChunks] = {}; bool failed = false; };
-  std::map<int, Dev> devs;
-  // nullptr: not served (the caller allocates normally)
-  void* take(size_t n, int* dev_out, int* chunk_out) {
-    if (n == 0 || n > ((size_t)1 << 20)) return nullptr;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> g(mu);
-    Dev& d = devs[dev];
-    if (d.failed) return nullptr;
-    if (!d.base && hipMalloc((void**)&d.base, kChunk * kChunks) != hipSuccess) {
-      d.base = nullptr;
-      d.failed = true;
-      return nullptr;
-    }
-    n = (n + 255) & ~(size_t)255;
-    if (d.off + n > kChunk) {
-      int k = 1;
-      while (k <= kChunks && d.live[(d.cur + k) % kChunks] != 0) ++k;
-      if (k > kChunks) return nullptr;
-      d.cur = (d.cur + k) % kChunks;
-      d.off = 0;
-    }
-    void* p = d.base + (size_t)d.cur * kChunk + d.off;
-    d.off += n;
-    ++d.live[d.cur];
-    *dev_out = dev;
-    *chunk_out = d.cur;
-    return p;
-  }
-  void put(int dev, int chunk) {
-    std::lock_guard<std::mutex> g(mu);
-    --devs[dev].live[chunk];
-  }
-};
-static UploadArena& upload_arena() {
-  static UploadArena* a = new UploadArena();  // never destroyed (like the pool)
-  return *a;
-}
-
 // set by pinot_amd_result_destroy while the result's members are destroyed (its stream synchronised)
 static thread_local bool g_release_to_pool = false;
-
-static bool upload_arena_on() {
-  static const bool on = []() {
-    const char* v = getenv("PINOT_AMD_UPLOAD_ARENA");
-    return v && strcmp(v, "1") == 0;
-  }();
-  return on;
-}
 
 struct DevBuf {
   void* p = nullptr;
@@ -252,15 +197,9 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   bool never_free = false;  // diagnostics (PINOT_AMD_DIAG_FRESH_UPLOADS): an upload's address is never reused
-  int arena_dev = -1, arena_chunk = -1;  // a slice of the upload arena
   void release() {
     if (p && never_free) p = nullptr;
     never_free = false;
-    if (p && arena_chunk >= 0) {
-      upload_arena().put(arena_dev, arena_chunk);
-      p = nullptr;
-    }
-    arena_chunk = arena_dev = -1;
     if (p && !(g_release_to_pool && bsz && dev_pool().put(p, bsz))) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -293,9 +232,6 @@ struct DevBuf {
         return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
       }
       never_free = true;
-    } else if (upload_arena_on() && (p = upload_arena().take(len + pad, &arena_dev, &arena_chunk))) {
-      n = len + pad;
-      bsz = 0;
     } else if (int rc = raw_alloc(len + pad)) {
       return rc;
     }
