@@ -4035,7 +4035,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
       }
       L.part.counts = (unsigned long long*)r->matched.p + 3 * li;
-      L.part.check = (unsigned long long*)r->matched.p + 3 * nl + 2;
+      // (PINOT_AMD_SCATTER_CHECK=0: no self-check -- A/B measurements)
+      L.part.check = env_is("PINOT_AMD_SCATTER_CHECK", "0") ? nullptr : (unsigned long long*)r->matched.p + 3 * nl + 2;
     } else if (jp.select) {
       // select pass: plain 256-thread blocks without LDS; gather pass: the table's block size and LDS
       L.select = true;
