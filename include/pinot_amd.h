@@ -279,6 +279,14 @@ int pinot_amd_result_fetch(pinot_amd_result* r, int64_t cap, int64_t* h_keys, do
 int pinot_amd_result_fetch_intermediate(pinot_amd_result* r, int64_t cap, double* h_pairs, int64_t* h_num_fetched);
 /* String value of merged-dictionary id `id` for group-by column j. */
 const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t id);
+/* The execution's self-check word (device address of one uint64; 0 = the check held). Partitioned plans
+ * verify that every doc past the filter became exactly one record and reached the aggregation
+ * (DefaultGroupByExecutor.java:192-219 folds each doc once); a nonzero word voids the result: every read
+ * of its groups or matched count fails with PINOT_AMD_EINVAL. A multi-GPU merge carries the word through
+ * its collectives (every rank then fails, none returns a table a failed rank contributed to). */
+int pinot_amd_result_check_word(pinot_amd_result* r, void** h_d_word);
+/* Executions of this process whose self-check failed (each also failed its result with PINOT_AMD_EINVAL). */
+int64_t pinot_amd_selfcheck_failures(void);
 /* Device view of the dense accumulators for a multi-GPU merge (RCCL all-reduce in place):
  * per aggregation slot an array of num_key_slots 8-byte words; op per slot: 0 = sum(int64),
  * 1 = sum(double), 2 = min(uint64 ordered), 3 = max(uint64 ordered), 4 / 5 = low / high word of an

@@ -93,6 +93,8 @@ SIGNATURES = {
     "pinot_amd_result_fetch_intermediate": (C.c_int, [_P, C.c_int64, C.POINTER(C.c_double), _I64P]),
     "pinot_amd_result_string_key": (C.c_char_p, [_P, C.c_int32, C.c_int64]),
     "pinot_amd_result_accumulators": (C.c_int, [_P, C.POINTER(C.c_int32), _I64P, _PP, C.POINTER(C.c_int32)]),
+    "pinot_amd_result_check_word": (C.c_int, [_P, _PP]),
+    "pinot_amd_selfcheck_failures": (C.c_int64, []),
     "pinot_amd_result_export_groups": (C.c_int, [_P, _P, _P, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                                  _I64P, _P]),
     "pinot_amd_result_merge_groups": (C.c_int, [_P, _P, _P, C.c_int64, _P]),

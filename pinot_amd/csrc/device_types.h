@@ -107,10 +107,17 @@ struct DevPartition {
   uint8_t* ovf_rec;          // overflow slab: records, their partitions, and the count
   uint32_t* ovf_part;
   unsigned long long* ovf_n;
-  // exact plans: incremented by every scatter block whose records in some partition end anywhere but where the
-  // count pass said they would (the host then runs the plan again)
+  // the execution's self-check word, 0 when it holds (the result then refuses its groups, PINOT_AMD_EINVAL):
+  // exact plans add every partition whose scatter-block run ends anywhere but where the count pass put the next
+  // block's records; sampled plans every scatter block whose records made (docs past the filter, numGroupsLimit
+  // admission and the segment trim) differ from the records it left in its allotments plus those it sent to the
+  // overflow slab
   unsigned long long* check;
+  // per block, 4 words: the HW_ID and XCC_ID hardware registers, the block's self-check mismatches, its records
+  // (count blocks at [4 * b], scatter blocks at [4 * (count grid + b)]): a failed check names the CUs involved
+  uint32_t* hw;
 };
+constexpr int kHwWords = 4;
 
 // Inverted-index leaf of one segment: the selected RoaringBitmap containers (of every dictId the
 // predicate selects) are OR-ed into a dense docId bitset (BitmapBasedFilterOperator's bitmap OR).

@@ -35,6 +35,7 @@ namespace pamd {
 hipError_t launch_init_acc(uint64_t* d_acc, const DevQuery& q, int64_t num_keys, hipStream_t st);
 hipError_t launch_sext_hi(uint64_t* d_acc, int64_t n, const int32_t* arrs, int32_t narr, hipStream_t st);
 hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long long* out, hipStream_t st);
+hipError_t launch_fingerprint(const void* p, size_t bytes, unsigned long long* out, hipStream_t st);
 hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, const uint64_t* acc, int fd_acc,
                        int32_t nsegs, int64_t limit, const int64_t* bucket_base, uint32_t* hist,
                        unsigned long long* seg_distinct, int64_t* bstar, int64_t* rank, unsigned long long* bitmap,
@@ -196,10 +197,7 @@ struct DevBuf {
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
-  bool never_free = false;  // diagnostics (PINOT_AMD_DIAG_FRESH_UPLOADS): an upload's address is never reused
   void release() {
-    if (p && never_free) p = nullptr;
-    never_free = false;
     if (p && !(g_release_to_pool && bsz && dev_pool().put(p, bsz))) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -223,18 +221,7 @@ struct DevBuf {
   // allocate n bytes + pad (zeroed), copy `src` (len bytes) to the front
   int alloc_copy(const void* src, size_t len, size_t pad) {
     release();
-    static const bool fresh = getenv("PINOT_AMD_DIAG_FRESH_UPLOADS") && atoi(getenv("PINOT_AMD_DIAG_FRESH_UPLOADS")) == 1;
-    if (fresh && len + pad <= ((size_t)1 << 20)) {
-      n = len + pad;
-      bsz = 0;
-      if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
-        p = nullptr;
-        return fail(PINOT_AMD_ENOMEM, "hipMalloc(%zu) failed", n);
-      }
-      never_free = true;
-    } else if (int rc = raw_alloc(len + pad)) {
-      return rc;
-    }
+    if (int rc = raw_alloc(len + pad)) return rc;
     if (!pad) {
       if (len) HIP_OK(hipMemcpy(p, src, len, hipMemcpyHostToDevice));
       else HIP_OK(hipMemset(p, 0, n));
@@ -262,6 +249,24 @@ struct DevBuf {
     return alloc(len);
   }
 };
+
+// Staged forward-index buffers and their device fingerprints at staging (launch_fingerprint): the partitioned plan's
+// self-check report compares them with the bytes' fingerprints at the failure (selfcheck_report).
+struct StagedPrint {
+  size_t bytes;
+  unsigned long long print;
+};
+static std::mutex g_print_mu;
+static std::map<const void*, StagedPrint> g_prints;
+
+static int device_fingerprint(const void* p, size_t bytes, unsigned long long* out) {
+  DevBuf h;
+  if (int rc = h.alloc(8)) return rc;
+  HIP_OK(hipMemset(h.p, 0, 8));
+  HIP_OK(launch_fingerprint(p, bytes, (unsigned long long*)h.p, nullptr));
+  HIP_OK(hipMemcpy(out, h.p, 8, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 static uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -812,6 +817,10 @@ static void drop_segment_caches(uint64_t uid);
 
 int pinot_amd_segment_destroy(pinot_amd_segment* seg) {
   if (seg) drop_segment_caches(seg->uid);  // merged key spaces and remaps over it (host.cpp key caches)
+  if (seg) {
+    std::lock_guard<std::mutex> g(g_print_mu);
+    for (auto& kv : seg->cols) g_prints.erase(kv.second->fwd.p);
+  }
   delete seg;
   return 0;
 }
@@ -961,6 +970,12 @@ int pinot_amd_segment_add_column(pinot_amd_segment* seg, const pinot_amd_column_
     if (rc) return rc;
   }
   seg->device_bytes += (int64_t)(c->fwd.n + c->dict.n + c->inv.n + c->inv_conts.n);
+  if (c->fwd.p) {
+    StagedPrint sp{c->fwd.n, 0};
+    if (int rc2 = device_fingerprint(c->fwd.p, sp.bytes, &sp.print)) return rc2;
+    std::lock_guard<std::mutex> g(g_print_mu);
+    g_prints[c->fwd.p] = sp;
+  }
   seg->cols[c->name] = std::move(c);
   return 0;
 }
@@ -1393,6 +1408,9 @@ struct pinot_amd_result {
   std::string jit_status;
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
+  bool check_failed = false;  // the last execution's partitioned self-check failed (verify_partitioned)
+  std::string check_msg;
+  DevBuf part_hw;  // per launch: the count and scatter blocks' placement and tallies (DevPartition::hw)
   DevBuf eff_begin, ovf_n, ovf_rec, ovf_part;  // sampled plans: allotment prefix, overflow slab
   // selection-vector plans: the shared vector (launches run one after another) and 2 counters per launch
   DevBuf sel, sel_ctr;
@@ -2080,66 +2098,6 @@ static int cached_remap(const pinot_amd_segment* s, const std::string& col, cons
 // ------------------------------------------------------------------------------------------------
 // execution
 // ------------------------------------------------------------------------------------------------
-// Diagnostics (PINOT_AMD_DIAG_SCATTER=1): FNV checksum of the forward-index bytes and the remaps of a launch's
-// segments (synchronises the stream): a plan must never change them
-static uint64_t diag_segment_sum(const Launch& L, hipStream_t st) {
-  uint64_t h = 0xcbf29ce484222325ull;
-  std::vector<DevSegment> ds(L.segs.size());
-  if (hipStreamSynchronize(st) != hipSuccess ||
-      hipMemcpy(ds.data(), L.d_segs.p, ds.size() * sizeof(DevSegment), hipMemcpyDeviceToHost) != hipSuccess)
-    return 0;
-  std::vector<uint8_t> buf;
-  for (const DevSegment& d : ds)
-    for (int c = 0; c < kMaxSlots; ++c) {
-      const DevColumn& col = d.cols[c];
-      if (!col.data) continue;
-      const size_t n = col.enc == ENC_FIXED_BIT ? (size_t)((d.num_docs * col.bits + 7) / 8)
-                       : col.enc == ENC_RAW ? (size_t)d.num_docs * (col.type == T_INT || col.type == T_FLOAT ? 4 : 8) : 0;
-      buf.resize(n);
-      if (n && hipMemcpy(buf.data(), col.data, n, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-      for (uint8_t b : buf) h = (h ^ b) * 0x100000001b3ull;
-      if (col.remap && col.card > 0) {
-        buf.resize((size_t)col.card * 4);
-        if (hipMemcpy(buf.data(), col.remap, buf.size(), hipMemcpyDeviceToHost) != hipSuccess) return 0;
-        for (uint8_t b : buf) h = (h ^ b) * 0x100000001b3ull;
-      }
-    }
-  return h;
-}
-
-// Diagnostics of an exact partitioned launch (PINOT_AMD_DIAG_SCATTER=1; the record buffer was filled with 0xFF
-// before the scatter): the records the scatter left unwritten, by partition and scatter block, to stderr.
-static void diag_scatter_report(const Launch& L, unsigned count_grid, hipStream_t st) {
-  const int P = L.part.nparts, R = L.rec_bytes, grid = L.grid;
-  std::vector<int64_t> pb((size_t)P + 1), offs((size_t)P * count_grid);
-  if (hipStreamSynchronize(st) != hipSuccess ||
-      hipMemcpy(pb.data(), L.part.part_begin, pb.size() * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(offs.data(), L.part.offs, offs.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
-    return;
-  const int64_t total = pb[P];
-  std::vector<uint8_t> rec((size_t)std::max<int64_t>(total, 0) * R);
-  if (total > 0 && hipMemcpy(rec.data(), L.part.rec, rec.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
-  int64_t unwritten = 0;
-  std::string ex;
-  for (int64_t i = 0; i < total; ++i) {
-    bool sentinel = true;
-    for (int b = 0; b < R && sentinel; ++b) sentinel = rec[(size_t)i * R + b] == 0xFF;
-    if (!sentinel) continue;
-    ++unwritten;
-    if (unwritten > 12) continue;
-    const int p = (int)(std::upper_bound(pb.begin(), pb.end(), i) - pb.begin()) - 1;
-    int64_t blk = 0;  // the scatter block whose run of partition p holds record i
-    for (int b = 0; b < grid; ++b)
-      if (pb[p] + offs[(size_t)p * count_grid + (size_t)b * kPartCountRatio] <= i) blk = b;
-    const int64_t run0 = pb[p] + offs[(size_t)p * count_grid + (size_t)blk * kPartCountRatio];
-    const int64_t run1 = blk + 1 < grid ? pb[p] + offs[(size_t)p * count_grid + (size_t)(blk + 1) * kPartCountRatio] : pb[p + 1];
-    ex += " [rec " + std::to_string(i) + " part " + std::to_string(p) + " block " + std::to_string(blk) + " run " +
-          std::to_string(run0) + ".." + std::to_string(run1) + " at " + std::to_string(i - run0) + "]";
-  }
-  fprintf(stderr, "DIAG_SCATTER records %lld unwritten %lld grid %d count_grid %u parts %d%s\n", (long long)total,
-          (long long)unwritten, grid, count_grid, P, ex.c_str());
-}
-
 static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table, const DevHash& H) {
   hipStream_t st = r->stream;
   const DevSegment* segs = (const DevSegment*)L.d_segs.p;
@@ -2190,10 +2148,8 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
     void* sargs[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&sampled, (void*)&L.part, (void*)&h};
     HIP_OK(hipMemsetAsync(L.part.ovf_n, 0, 8, st));
     HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem, st, sargs, nullptr));
-    static const double cap_scale = []() {
-      const char* v = getenv("PINOT_AMD_PART_CAP_SCALE");  // tests: < 1 forces records into the slab
-      return v ? std::max(0.0, atof(v)) : 1.0;
-    }();
+    const char* cs = getenv("PINOT_AMD_PART_CAP_SCALE");  // tests: < 1 forces records into the slab
+    const double cap_scale = cs ? std::max(0.0, atof(cs)) : 1.0;
     HIP_OK(launch_allot_prefix(L.part.hist, L.part.nparts, L.grid, 0, L.part.sample_stride, cap_scale, L.region_cap,
                                L.part.part_begin, L.part.offs, st));
     if (L.jit_atomic)
@@ -2216,22 +2172,11 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
   HIP_OK(launch_partition_offsets(L.part.hist, L.part.nparts, count_grid, L.part.offs, L.part.part_begin, st));
   if (L.jit_atomic)
     HIP_OK(hipModuleLaunchKernel(L.jit_atomic->fn, (unsigned)L.atomic_grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
-  // diagnostics (PINOT_AMD_DIAG_SCATTER=1): records the scatter leaves unwritten (a sentinel fill before it)
-  static const bool diag_scatter = env_is("PINOT_AMD_DIAG_SCATTER", "1");
-  const size_t rec_fill = (size_t)L.docs * (size_t)L.rec_bytes;
-  if (diag_scatter) HIP_OK(hipMemsetAsync(L.part.rec, 0xFF, rec_fill, st));
-  const uint64_t diag_sum0 = diag_scatter ? diag_segment_sum(L, st) : 0;  // (before the scatter: after count + offsets)
   HIP_OK(hipModuleLaunchKernel(L.jit->fn_scatter, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem_scatter, st, args,
                                nullptr));
   void* agg_args[] = {(void*)&L.part, (void*)&table};
   HIP_OK(hipModuleLaunchKernel(L.jit->fn_agg, (unsigned)L.agg_grid, 1, 1, 1024, 1, 1, (unsigned)L.shmem_agg, st,
                                agg_args, nullptr));
-  if (diag_scatter) {  // (after the aggregation: the same kernel sequence)
-    diag_scatter_report(L, count_grid, st);
-    const uint64_t s2 = diag_segment_sum(L, st);
-    if (s2 != diag_sum0) fprintf(stderr, "DIAG_SEGSUM changed during the plan: %016llx -> %016llx\n",
-                                 (unsigned long long)diag_sum0, (unsigned long long)s2);
-  }
   return 0;
 }
 
@@ -2390,6 +2335,7 @@ static int grow_hash(pinot_amd_result* r, bool* grown) {
 
 static int run_plan(pinot_amd_result* r) {
   r->merged = false;
+  r->check_failed = false;
   r->ovf_pending = false;
   hipStream_t st = r->stream;
   r->compacted = false;
@@ -3830,11 +3776,14 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // (default-limit configs[3] scatter: 20.1 -> 8.8 GB fetched per 400M rows, 4.87 -> 4.15 ms per plan;
       // profiles/r05/pmc_hcdef_xcd.txt). PINOT_AMD_XCD_REMAP=0|1 pins it.
       jp.xcd_remap = env_is("PINOT_AMD_XCD_REMAP", "1") || (jp.admit && !env_is("PINOT_AMD_XCD_REMAP", "0"));
+#ifdef PINOT_AMD_DIAGNOSTICS
+      // measurement-only variants that void the results (round-5 profiles): built with -DPINOT_AMD_DIAGNOSTICS only
       jp.diag_admit_off = env_is("PINOT_AMD_DIAG_ADMIT_OFF", "1");
       if (jp.partitioned) {
         const int64_t w = env_i64("PINOT_AMD_DIAG_REC_WRAP", 0);
         jp.diag_rec_wrap = (w >= 4096 && (w & (w - 1)) == 0) ? w : 0;
       }
+#endif
     }
     if (jp.partitioned) {
       jit_layout_records(&jp);
@@ -4035,8 +3984,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
         L.sample_grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * ns, (vt + 3) / 4));
       }
       L.part.counts = (unsigned long long*)r->matched.p + 3 * li;
-      // (PINOT_AMD_SCATTER_CHECK=0: no self-check -- A/B measurements)
-      L.part.check = env_is("PINOT_AMD_SCATTER_CHECK", "0") ? nullptr : (unsigned long long*)r->matched.p + 3 * nl + 2;
+      L.part.check = (unsigned long long*)r->matched.p + 3 * nl + 2;
     } else if (jp.select) {
       // select pass: plain 256-thread blocks without LDS; gather pass: the table's block size and LDS
       L.select = true;
@@ -4111,6 +4059,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     if (int rc = r->offs.alloc(max_count_cells * 8)) return rc;
     if (int rc = r->part_begin.alloc(((size_t)maxp + 1) * 8)) return rc;
     if (int rc = r->rec.alloc(max_rec)) return rc;
+    int64_t hw_blocks = 0;  // per launch: count grid + scatter grid entries
+    for (auto& L : r->launches) hw_blocks = std::max<int64_t>(hw_blocks, (int64_t)L.grid * (kPartCountRatio + 1));
+    if (int rc = r->part_hw.alloc((size_t)hw_blocks * r->launches.size() * kHwWords * 4)) return rc;
+    HIP_OK(hipMemset(r->part_hw.p, 0, r->part_hw.n));
+    for (size_t li = 0; li < r->launches.size(); ++li)
+      r->launches[li].part.hw = (uint32_t*)r->part_hw.p + (size_t)li * hw_blocks * kHwWords;
     if (max_slab > 0) {
       if (int rc = r->eff_begin.alloc(max_count_cells * 8 + 8)) return rc;
       if (int rc = r->ovf_n.alloc(8)) return rc;
@@ -4332,26 +4286,144 @@ static int read_counters(pinot_amd_result* r, std::vector<unsigned long long>* c
   return 0;
 }
 
-// A partitioned execution whose scatter disagreed with its count pass (some block's records short of or past its
-// counted runs -- measured as a transient misread of one block's tiles on the round-5 boxes) is run
-// again, up to three times; *c is re-read after each run.
-static int settle_partitioned(pinot_amd_result* r, std::vector<unsigned long long>* c) {
-  for (int retry = 0; r->kind == PLAN_PARTITIONED && (*c)[3 * r->launches.size() + 2] != 0; ++retry) {
-    if (retry == 3)
-      return fail(PINOT_AMD_EINVAL, "partitioned scatter disagreed with its count pass in %d executions", retry + 1);
-    fprintf(stderr, "pinot_amd: partitioned scatter disagreed with its count pass (%llu partition runs); "
-            "running the plan again\n", (unsigned long long)(*c)[3 * r->launches.size() + 2]);
-    if (int rc = run_plan(r)) return rc;
-    if (int rc = read_counters(r, c)) return rc;
+// Executions whose partitioned self-check failed, process-wide (pinot_amd_selfcheck_failures): the test suite fails
+// its session on a nonzero count, so a caller that swallowed the error still shows up.
+static std::atomic<long long> g_selfcheck_failures{0};
+
+// One line per scatter block that failed the partitioned self-check: its hardware placement (XCC, SE, SH, CU from
+// HW_ID / XCC_ID), the records it made and the records its count blocks counted (exact plans), and where those
+// count blocks ran -- the evidence a failure leaves, whichever process hits it.
+static std::string selfcheck_report(pinot_amd_result* r) {
+  std::string out;
+  for (size_t li = 0; li < r->launches.size(); ++li) {
+    const Launch& L = r->launches[li];
+    if (!L.part.hw || L.grid <= 0) continue;
+    const int64_t cg = (int64_t)L.grid * kPartCountRatio, P = L.part.nparts;
+    std::vector<uint32_t> hw((size_t)(cg + L.grid) * kHwWords);
+    if (hipMemcpy(hw.data(), L.part.hw, hw.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) continue;
+    std::vector<uint32_t> hist;  // (the launches share the histogram buffer: it holds the last launch's)
+    if (!L.part_sampled && li + 1 == r->launches.size()) {
+      hist.resize((size_t)P * cg);
+      if (hipMemcpy(hist.data(), L.part.hist, hist.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) hist.clear();
+    }
+    auto where = [&](int64_t e) {
+      const uint32_t id = hw[(size_t)e * kHwWords], x = hw[(size_t)e * kHwWords + 1];
+      char b[96];
+      snprintf(b, sizeof(b), "xcc %u se %u sh %u cu %u", x, (id >> 13) & 7u, (id >> 12) & 1u, (id >> 8) & 15u);
+      return std::string(b);
+    };
+    int shown = 0;
+    for (int64_t b = 0; b < L.grid && shown < 8; ++b) {
+      const int64_t e = cg + b;
+      if (hw[(size_t)e * kHwWords + 2] == 0) continue;
+      ++shown;
+      char line[256];
+      snprintf(line, sizeof(line), "\n  launch %zu scatter block %lld (%s): %u %s, %u records made", li, (long long)b,
+               where(e).c_str(), hw[(size_t)e * kHwWords + 2], L.part_sampled ? "records unaccounted" : "partition runs off",
+               hw[(size_t)e * kHwWords + 3]);
+      out += line;
+      if (!hist.empty()) {
+        int64_t counted = 0;
+        for (int64_t c = b * kPartCountRatio; c < (b + 1) * kPartCountRatio && c < cg; ++c) {
+          for (int64_t q = 0; q < P; ++q) counted += hist[(size_t)q * cg + c];
+          out += "; count block " + std::to_string(c) + " (" + where(c) + ")";
+        }
+        out += "; counted " + std::to_string(counted);
+      }
+    }
+    // the columns' HBM bytes against their fingerprints at staging: changed bytes vs a misread of intact ones
+    std::vector<DevSegment> ds(L.segs.size());
+    if (!ds.empty() &&
+        hipMemcpy(ds.data(), L.d_segs.p, ds.size() * sizeof(DevSegment), hipMemcpyDeviceToHost) == hipSuccess) {
+      int checked = 0, changed = 0;
+      std::string which;
+      for (size_t k = 0; k < ds.size(); ++k)
+        for (int c = 0; c < kMaxSlots; ++c) {
+          const void* d = ds[k].cols[c].data;
+          StagedPrint sp{};
+          {
+            std::lock_guard<std::mutex> g(g_print_mu);
+            auto it = g_prints.find(d);
+            if (!d || it == g_prints.end()) continue;
+            sp = it->second;
+          }
+          unsigned long long now = 0;
+          if (device_fingerprint(d, sp.bytes, &now)) continue;
+          ++checked;
+          if (now != sp.print) {
+            ++changed;
+            if (changed <= 4) which += " (segment " + std::to_string(k) + " slot " + std::to_string(c) + ")";
+          }
+        }
+      out += "\n  launch " + std::to_string(li) + ": " + std::to_string(changed) + " of " + std::to_string(checked) +
+             " staged column buffers changed since staging" + which;
+    }
+    // the count pass run again on the same inputs (exact plans): does it reproduce its first histogram?
+    if (!L.part_sampled && !hist.empty()) {
+      DevBuf h2, m2, hw2;
+      if (h2.alloc(hist.size() * 4) || m2.alloc(64) || hw2.alloc((size_t)cg * kHwWords * 4)) continue;
+      (void)hipMemset(m2.p, 0, 64);
+      DevPartition pc = L.part;
+      pc.hist = (uint32_t*)h2.p;
+      pc.hw = (uint32_t*)hw2.p;
+      const DevSegment* segs = (const DevSegment*)L.d_segs.p;
+      uint64_t* table = nullptr;
+      uint64_t* const* bits = nullptr;
+      unsigned long long* matched = (unsigned long long*)m2.p;
+      DevHash h{};
+      DevQuery q = L.q;
+      void* args[] = {(void*)&segs, (void*)&q, (void*)&table, (void*)&bits, (void*)&matched, (void*)&pc, (void*)&h};
+      std::vector<uint32_t> again(hist.size());
+      if (hipModuleLaunchKernel(L.jit->fn, (unsigned)cg, 1, 1, (unsigned)(kBlock * L.part_sub), 1, 1, (unsigned)L.shmem,
+                                nullptr, args, nullptr) != hipSuccess ||
+          hipMemcpy(again.data(), h2.p, again.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        continue;
+      int64_t cells = 0, blocks = 0;
+      std::string ex;
+      for (int64_t c = 0; c < cg; ++c) {
+        int64_t d = 0, t1 = 0, t2 = 0;
+        for (int64_t q2 = 0; q2 < P; ++q2) {
+          const size_t i = (size_t)q2 * cg + c;
+          d += hist[i] != again[i];
+          t1 += hist[i];
+          t2 += again[i];
+        }
+        cells += d;
+        if (d) {
+          ++blocks;
+          if (blocks <= 4)
+            ex += " (count block " + std::to_string(c) + ": " + std::to_string(t1) + " -> " + std::to_string(t2) + ")";
+        }
+      }
+      out += "\n  launch " + std::to_string(li) + ": the count pass run again differs in " + std::to_string(cells) +
+             " cells of " + std::to_string(blocks) + " count blocks" + ex;
+    }
   }
-  return 0;
+  return out;
+}
+
+// A partitioned execution whose self-check failed (DevPartition::check) fails its result: its groups and matched
+// counts are never read. There is no re-execution: the cause of the round-5 misreads is gone (module loads, jit.cpp
+// jit_get), and any future failure must surface, with the blocks' placement, instead of being retried away.
+static int verify_partitioned(pinot_amd_result* r, const std::vector<unsigned long long>& c) {
+  if (r->kind != PLAN_PARTITIONED || r->check_failed) return r->check_failed ? fail(PINOT_AMD_EINVAL, "%s", r->check_msg.c_str()) : 0;
+  const unsigned long long bad = c[3 * r->launches.size() + 2];
+  if (bad == 0) return 0;
+  r->check_failed = true;
+  ++g_selfcheck_failures;
+  r->check_msg = "partitioned plan self-check failed (" + std::to_string(bad) +
+                 (r->launches.empty() || !r->launches[0].part_sampled ? " partition runs off their counted records"
+                                                                       : " scatter blocks with unaccounted records") +
+                 "); the result is void" + selfcheck_report(r);
+  fprintf(stderr, "pinot_amd: %s\n", r->check_msg.c_str());
+  return fail(PINOT_AMD_EINVAL, "%s", r->check_msg.c_str());
 }
 
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out) {
   if (!r || !h_out) return fail(PINOT_AMD_EINVAL, "num_docs_matched: bad arguments");
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
-  if (int rc = settle_partitioned(r, &c)) return rc;
+  if (int rc = verify_partitioned(r, c)) return rc;
   // per launch: the scan / count pass and the direct-atomic scan both count every matching doc;
   // whichever ran has the total (partitioned plans run one of them)
   int64_t total = 0;
@@ -4441,7 +4513,7 @@ static int check_overflow(pinot_amd_result* r) {
       }
     }
   }
-  if (int rc = settle_partitioned(r, &c)) return rc;
+  if (int rc = verify_partitioned(r, c)) return rc;
   if (c[3 * r->launches.size() + 1] != 0)
     return fail(PINOT_AMD_EOVERFLOW, "group hash table full (%lld docs without a slot); raise PINOT_AMD_HASH_TABLE_BYTES",
                 (long long)c[3 * r->launches.size() + 1]);
@@ -4831,6 +4903,14 @@ const char* pinot_amd_result_string_key(pinot_amd_result* r, int32_t j, int64_t 
   if (m.type != T_STRING || id < 0 || id >= (int64_t)m.vs.size()) return nullptr;
   return m.vs[id].c_str();
 }
+
+int pinot_amd_result_check_word(pinot_amd_result* r, void** h_d_word) {
+  if (!r || !h_d_word) return fail(PINOT_AMD_EINVAL, "check_word: bad arguments");
+  *h_d_word = (unsigned long long*)r->matched.p + 3 * r->launches.size() + 2;
+  return 0;
+}
+
+int64_t pinot_amd_selfcheck_failures(void) { return (int64_t)g_selfcheck_failures.load(); }
 
 int pinot_amd_result_accumulators(pinot_amd_result* r, int32_t* h_num_slots, int64_t* h_num_key_slots,
                                   void** h_slot_ptrs, int32_t* h_slot_ops) {

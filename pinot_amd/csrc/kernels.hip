@@ -1601,6 +1601,31 @@ __global__ void raw_int_minmax_kernel(const uint8_t* __restrict__ be, int type, 
   }
 }
 
+// Order-independent 64-bit fingerprint of a device buffer (word i mixed with its index, summed): taken when a column
+// is staged and again when a partitioned plan's self-check fails, it tells a column whose HBM bytes changed since
+// staging apart from a misread of intact bytes (host.cpp selfcheck_report).
+__global__ void fingerprint_kernel(const uint64_t* p, int64_t nwords, unsigned long long* out) {
+  uint64_t h = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t x = p[i] ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    h += x;
+  }
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  if ((threadIdx.x & 63) == 0 && h) atomicAdd(out, (unsigned long long)h);
+}
+
+hipError_t launch_fingerprint(const void* p, size_t bytes, unsigned long long* out, hipStream_t st) {
+  const int64_t nw = (int64_t)(bytes / 8);
+  if (nw <= 0) return hipSuccess;
+  unsigned g = grid_for(nw, kBlock);
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(g), dim3(kBlock), 0, st, (const uint64_t*)p, nw, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_raw_int_minmax(const uint8_t* be, int type, int64_t n, long long* out, hipStream_t st) {
   unsigned g = grid_for(n, kBlock);
   if (g > 2048) g = 2048;

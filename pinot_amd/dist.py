@@ -99,7 +99,8 @@ def _reduce_gathered(g, ops):
     return out
 
 
-def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_max_bytes: int = 1 << 20) -> int:
+def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_max_bytes: int = 1 << 20,
+                 check=None) -> int:
     """In-place merge across ranks of a [len(ops), num_keys] int64 tensor of accumulator words.
 
     ops per row: 0 = int64 sum, 1 = fp64 sum (words are double bits), 2/3 = min/max of the
@@ -110,6 +111,9 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_ma
     (a latency-bound exchange: one collective instead of one per reduction kind). Larger tables: one
     all-reduce per reduction kind (integer sums incl. the limbs of 128-bit rows in one int64 SUM, double
     sums in one fp64 SUM, one MIN, one MAX), each moving ~2x the table per rank on a ring.
+    `check`: None, or a 1-element int64 tensor (the result's self-check word, engine.QueryResult.check_word)
+    merged in the same collectives (max / sum, both nonzero iff some rank's is): a rank whose execution
+    failed its self-check then voids every rank's merged table, with no extra collective and no host read.
     Returns the bytes this rank put into the collectives."""
     import torch
     import torch.distributed as dist
@@ -119,20 +123,30 @@ def merge_tables(table, ops: Sequence[int], num_keys: int, group=None, gather_ma
     if world == 1:
         return 0
     if t.numel() * 8 <= gather_max_bytes:
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t.contiguous(), group=group)
-        t.copy_(_reduce_gathered(torch.stack(parts), ops))
-        return t.numel() * 8
+        src = t.contiguous() if check is None else torch.cat([t.reshape(-1), check.reshape(1)])
+        parts = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(parts, src, group=group)
+        g = torch.stack(parts)
+        if check is not None:
+            check.copy_(g[:, -1].max().reshape(check.shape))
+            g = g[:, :-1].reshape(world, len(ops), num_keys)
+        t.copy_(_reduce_gathered(g, ops))
+        return src.numel() * 8
     nbytes = 0
     i64 = [i for i, op in enumerate(ops) if op == OP_SUM_I64]
     i128 = [i for i, op in enumerate(ops) if op == OP_SUM_I128]
     f64 = [i for i, op in enumerate(ops) if op == OP_SUM_F64]
     parts = [t[i64]] if i64 else []
     parts += [_limbs(t[i], t[i + 1]) for i in i128]
-    if parts:
-        buf = torch.cat(parts).contiguous()
+    if parts or check is not None:
+        rows = torch.cat(parts) if parts else t.new_empty((0, num_keys))
+        # the self-check word rides the integer sum as one extra element: summed, it is nonzero iff some rank's is
+        buf = rows.reshape(-1) if check is None else torch.cat([rows.reshape(-1), check.reshape(1)])
         nbytes += buf.numel() * 8
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        if check is not None:
+            check.copy_(buf[-1:].reshape(check.shape))
+        buf = buf[:rows.numel()].view(rows.shape)
         if i64:
             t[i64] = buf[:len(i64)]
         for j, i in enumerate(i128):
@@ -204,6 +218,16 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
         by_value, reached_any = (bool(x) for x in flag.tolist())
         scratch = {"result": result, "by_value": by_value, "reached": reached_any}
     by_value, reached_any = scratch["by_value"], scratch["reached"]
+    if by_value:
+        # the merge by value reads each rank's groups, and a result whose self-check failed refuses them: the ranks
+        # agree first, so every rank fails together instead of some waiting in a collective for a rank that raised
+        bad = any(p.self_check_failed() for p in parts if hasattr(p, "self_check_failed"))
+        flag = torch.tensor([1 if bad else 0], dtype=torch.int64,
+                            device="cuda" if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            raise RuntimeError("merge_result: a rank's execution failed its partitioned self-check; the merged "
+                               "result would be void on every rank")
     stats = {"path": None, "bytes": 0}
     for p in parts:
         if hasattr(p, "set_merged_limit_reached"):
@@ -217,7 +241,8 @@ def merge_result(result, scratch=None, group=None, stream=None, gather_max_bytes
             continue
         table = torch.as_tensor(_DeviceWords(ptrs[0], len(ops) * nk), device="cuda")
         assert table.data_ptr() == ptrs[0], "zero-copy view of the accumulator table failed"
-        stats["bytes"] += merge_tables(table, ops, nk, group, gather_max_bytes)
+        chk = torch.as_tensor(_DeviceWords(p.check_word(), 1), device="cuda") if hasattr(p, "check_word") else None
+        stats["bytes"] += merge_tables(table, ops, nk, group, gather_max_bytes, check=chk)
         stats["path"] = stats["path"] or ("dense-gather" if len(ops) * nk * 8 <= gather_max_bytes else "dense-allreduce")
     scratch["stats"] = stats
     return scratch

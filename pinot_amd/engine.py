@@ -209,6 +209,19 @@ class DistinctCountResult:
             r.destroy()
 
 
+class _DeviceWord:
+    """One library-owned int64 in HBM seen by torch without a copy (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int):
+        self.__cuda_array_interface__ = {"shape": (1,), "typestr": "<i8", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+def selfcheck_failures() -> int:
+    """Executions of this process whose partitioned self-check failed (pinot_amd_selfcheck_failures)."""
+    return int(lib().pinot_amd_selfcheck_failures())
+
+
 class QueryResult:
     """Results of one executed query plan (kept in HBM until fetched)."""
 
@@ -273,6 +286,20 @@ class QueryResult:
         ops = (C.c_int32 * n.value)()
         check(lib().pinot_amd_result_accumulators(self._h, C.byref(n), C.byref(nk), ptrs, ops), "accumulators")
         return list(ops), nk.value, [int(p) for p in ptrs]
+
+    def check_word(self) -> int:
+        """Device address of the execution's self-check word (one int64, 0 = the check held; see
+        pinot_amd_result_check_word): a cross-rank merge carries it through its collectives."""
+        out = C.c_void_p()
+        check(lib().pinot_amd_result_check_word(self._h, C.byref(out)), "check_word")
+        return int(out.value)
+
+    def self_check_failed(self) -> bool:
+        """Whether the last execution's self-check failed (reads the word without raising: the ranks of a
+        merge agree on it before anyone fails)."""
+        import torch
+        w = torch.as_tensor(_DeviceWord(self.check_word()), device="cuda")
+        return bool(int(w.item()) != 0)
 
     def has_dense_table(self) -> bool:
         """True when the groups live in a dense accumulator table over the key space (mergeable in place

@@ -17,6 +17,11 @@ SV_FILTER = (" WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 100000
              " AND (column6 < 500000000 OR column11 NOT IN ('t', 'P')) AND daysSinceEpoch = 126164076")
 
 
+# Partitioned-plan self-check failures the suite injects on purpose (test_gpu_selfcheck.py adds to it; the
+# conftest's session check compares the library's process-wide count with it)
+EXPECTED_SELFCHECK_FAILURES = [0]
+
+
 def load_expected():
     with open(os.path.join(GOLDEN, "sv_queries_expected.json")) as f:
         return json.load(f)
