@@ -121,6 +121,56 @@ static int fail(int code, const char* fmt, ...) {
 
 namespace {
 
+// Runtime knobs. A default build reads only the planner overrides the test suite exercises and the server's resource
+// limits (the list below); the experiment knobs of earlier rounds' sweeps (DESIGN.md records their outcomes) are
+// honoured only in a diagnostics build (-DPINOT_AMD_DIAGNOSTICS), so a default build plans from the query alone.
+static const char* knob(const char* name) {
+#ifndef PINOT_AMD_DIAGNOSTICS
+  static const std::set<std::string> kept = {
+      "PINOT_AMD_ADMIT_PREFIX",
+      "PINOT_AMD_ADMIT_SEQ",
+      "PINOT_AMD_ATOMIC_HANDOVER",
+      "PINOT_AMD_FILTER_GATE",
+      "PINOT_AMD_FLUSH_EVERY",
+      "PINOT_AMD_FLUSH_GROUP",
+      "PINOT_AMD_FUSED_INV_SELECT",
+      "PINOT_AMD_GENERIC_BITS",
+      "PINOT_AMD_GROUP_PLAN",
+      "PINOT_AMD_HASH_CAP_CACHE",
+      "PINOT_AMD_HASH_INIT_SLOTS",
+      "PINOT_AMD_HASH_LDS",
+      "PINOT_AMD_HASH_LDS_ADMIT",
+      "PINOT_AMD_HASH_LDS_SLOTS",
+      "PINOT_AMD_HASH_MAX_PROBE",
+      "PINOT_AMD_HASH_SPILL",
+      "PINOT_AMD_HASH_TABLE_BYTES",
+      "PINOT_AMD_INV_POLICY",
+      "PINOT_AMD_NARROW_SUMS",
+      "PINOT_AMD_PARTITIONED",
+      "PINOT_AMD_PART_CAP_SCALE",
+      "PINOT_AMD_PREFETCH",
+      "PINOT_AMD_SAMPLE_STRIDE",
+      "PINOT_AMD_SCAN_GROUP",
+      "PINOT_AMD_SELECT",
+      "PINOT_AMD_SELECT_PARTITIONED",
+      "PINOT_AMD_SEL_GROUP",
+      "PINOT_AMD_SPILL_BYTES",
+      "PINOT_AMD_SPILL_SORT",
+      "PINOT_AMD_STAGE_CAP",
+      "PINOT_AMD_TRIM_PLAN",
+      "PINOT_AMD_WIDE_LDS",
+      "PINOT_AMD_POOL_BYTES",
+      "PINOT_AMD_KEY_CACHE_BYTES",
+      "PINOT_AMD_SPILL_MAX_BYTES",
+      "PINOT_AMD_HASH_FINAL_MAX_BYTES",
+      "PINOT_AMD_ADMIT_MAX_BYTES",
+      "PINOT_AMD_DENSE_MAX_KEYS",
+  };
+  if (!kept.count(name)) return nullptr;
+#endif
+  return getenv(name);
+}
+
 // ------------------------------------------------------------------------------------------------
 // device buffers
 // ------------------------------------------------------------------------------------------------
@@ -137,7 +187,7 @@ struct DevPool {
   std::map<int, size_t> bytes;
   size_t cap = 0;
   DevPool() {
-    const char* e = getenv("PINOT_AMD_POOL_BYTES");
+    const char* e = knob("PINOT_AMD_POOL_BYTES");
     cap = e ? (size_t)strtoull(e, nullptr, 10) : ((size_t)1 << 30);
   }
   static size_t block_size(size_t n) {  // size classes: powers of two to 4 MiB, 1 MiB steps above
@@ -1584,7 +1634,7 @@ static void dict_range_of(const PredSpec& p, const Column& c, int64_t* start, in
 // aggregation). PINOT_AMD_INV_POLICY=always|never overrides (tests).
 static bool use_inverted_for(const Column& c, int64_t num_docs, const std::vector<int32_t>& ids, bool is_range,
                              int64_t start, int64_t end, bool decoded_anyway) {
-  if (const char* pol = getenv("PINOT_AMD_INV_POLICY")) {
+  if (const char* pol = knob("PINOT_AMD_INV_POLICY")) {
     if (strcmp(pol, "always") == 0) return true;
     if (strcmp(pol, "never") == 0) return false;
   }
@@ -1813,7 +1863,7 @@ constexpr size_t kLeafCacheMax = 256;  // entries per segment (cleared when full
 // make_leaf_uncached through the segment's leaf cache. The key is everything the resolution reads: the
 // predicate, the slot, whether its column is decoded anyway, and the knobs of the inverted-index policy.
 static std::string leaf_cache_key(const PredSpec& p, int slot, bool decoded_anyway) {
-  const char* pol = getenv("PINOT_AMD_INV_POLICY");
+  const char* pol = knob("PINOT_AMD_INV_POLICY");
   return preds_signature({p}) + "|" + std::to_string(slot) + "|" + (decoded_anyway ? "1" : "0") + "|" +
          std::to_string(expand_group()) + "|" + (pol ? pol : "");
 }
@@ -1998,7 +2048,7 @@ static int build_merged_keys(const std::vector<pinot_amd_segment*>& segs, const 
   ent.bytes = (*out)->host_bytes() + key.size();
   for (auto* sg : segs) ent.uids.push_back(sg->uid);
   static const size_t budget = []() {
-    const char* v = getenv("PINOT_AMD_KEY_CACHE_BYTES");
+    const char* v = knob("PINOT_AMD_KEY_CACHE_BYTES");
     return v ? (size_t)std::max(0ll, atoll(v)) : (size_t)1 << 30;
   }();
   std::lock_guard<std::mutex> g(g_keys_mu);
@@ -2114,7 +2164,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
     else
       // (select kernels hold their tables in static LDS)
       HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock, 1, 1, 0, st, args, nullptr));
-    if (getenv("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
+    if (knob("PINOT_AMD_CHECK_SELECT")) {  // diagnostics: validate the vector on the host
       unsigned long long ctr[2];
       HIP_OK(hipMemcpyAsync(ctr, L.q.sel_count, 16, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
@@ -2148,7 +2198,7 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
     void* sargs[] = {(void*)&segs, (void*)&L.q, (void*)&table, (void*)&bits, (void*)&sampled, (void*)&L.part, (void*)&h};
     HIP_OK(hipMemsetAsync(L.part.ovf_n, 0, 8, st));
     HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, pt, 1, 1, (unsigned)L.shmem, st, sargs, nullptr));
-    const char* cs = getenv("PINOT_AMD_PART_CAP_SCALE");  // tests: < 1 forces records into the slab
+    const char* cs = knob("PINOT_AMD_PART_CAP_SCALE");  // tests: < 1 forces records into the slab
     const double cap_scale = cs ? std::max(0.0, atof(cs)) : 1.0;
     HIP_OK(launch_allot_prefix(L.part.hist, L.part.nparts, L.grid, 0, L.part.sample_stride, cap_scale, L.region_cap,
                                L.part.part_begin, L.part.offs, st));
@@ -2181,11 +2231,11 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
 }
 
 static int64_t env_i64(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
+  const char* v = knob(name);
   return v ? atoll(v) : dflt;
 }
 static bool env_is(const char* name, const char* val) {
-  const char* v = getenv(name);
+  const char* v = knob(name);
   return v && strcmp(v, val) == 0;
 }
 
@@ -2850,7 +2900,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       const double sel = (!seg_matched.empty() && nd > 0) ? std::max((double)seg_matched[si] / (double)nd, 1e-9) : 1.0;
       const double rows = 2.0 * need / sel + 65536.0;
       int64_t pfx = rows >= (double)nd ? nd : ((int64_t)rows + kTileDocs - 1) / kTileDocs * kTileDocs;
-      if (const char* e = getenv("PINOT_AMD_ADMIT_PREFIX")) pfx = std::min<int64_t>(nd, std::max<int64_t>(kTileDocs, atoll(e)));
+      if (const char* e = knob("PINOT_AMD_ADMIT_PREFIX")) pfx = std::min<int64_t>(nd, std::max<int64_t>(kTileDocs, atoll(e)));
       r->a_prefix[si] = std::min(pfx, nd);
     }
   };
@@ -3320,7 +3370,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   auto slot_bpr = [](const DevColumn& c) -> double {
     return c.enc == ENC_FIXED_BIT ? c.bits / 8.0 : c.enc == ENC_RAW ? (double)value_size(c.type) : 0.0;
   };
-  const char* sel_env = getenv("PINOT_AMD_SELECT");
+  const char* sel_env = knob("PINOT_AMD_SELECT");
   // (a partitioned plan qualifies too: when its filter keeps few docs, the gather adds them straight into
   // the HBM table, where the partitioned plan would hand over to a fused direct-atomic scan of every row)
   const bool sel_eligible = !filter_only && q.nacc > 0 && np > 0 && !r->trim && !r->admit && !r->seg_trim &&
@@ -3761,12 +3811,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       jp.depth = bpr <= 0 ? 1 : (int)std::min(4.0, std::max(1.0, std::ceil(4096.0 / (256.0 * bpr))));
       // a select step of G tiles loads G tiles per register set: the same bytes in flight with 1/G the sets
       if (jp.sel_group > 1) jp.depth = std::max(1, (jp.depth + jp.sel_group - 1) / jp.sel_group);
-      if (const char* pd = getenv("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
+      if (const char* pd = knob("PINOT_AMD_PREFETCH")) jp.depth = std::max(1, std::min(8, atoi(pd)));
       if (env_is("PINOT_AMD_LANE_TABLES", "0")) {
         for (auto& js : jp.slots) js.dict_regs = 0;
         for (auto& jl : jp.leaves) jl.bits_regs = 0;
       }
-      if (const char* pw = getenv("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
+      if (const char* pw = knob("PINOT_AMD_WAVES_PER_EU")) jp.waves_per_eu = std::max(0, std::min(8, atoi(pw)));
       // non-temporal column loads for wide-row fused scans (configs[1]: 3.58 -> 3.51 ms per 1B rows); the
       // narrow SSB select passes measured 1-3 % slower with them, the partitioned scatter 10 % slower
       jp.nt_loads = env_is("PINOT_AMD_NT_LOADS", "1") ||
@@ -3805,7 +3855,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       int cap = 64;
       while (cap >= 4 && jit_scatter_lds(jp, cap) > stage_lds) --cap;
       jp.stage_cap = cap >= 4 ? cap : 0;
-      if (const char* sc = getenv("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
+      if (const char* sc = knob("PINOT_AMD_STAGE_CAP")) jp.stage_cap = std::min(jp.stage_cap, atoi(sc));
       jp.flush_pct = (int)std::min<int64_t>(100, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_PCT", 85)));
       jp.flush_every = (int)std::min<int64_t>(64, std::max<int64_t>(1, env_i64("PINOT_AMD_FLUSH_EVERY", 1)));
       jp.flush_par = !env_is("PINOT_AMD_FLUSH_PAR", "0");
@@ -3837,7 +3887,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // gated plans: column loads D tiles ahead of their gate, gate words 2D ahead. Measured on the
       // inverted-index sweep, deeper pipelines only add registers (the gated loop is bound by its
       // per-tile overhead, not by load latency), so the row-width depth stays unless overridden.
-      if (L.gated && getenv("PINOT_AMD_GATE_DEPTH"))
+      if (L.gated && knob("PINOT_AMD_GATE_DEPTH"))
         jp.depth = (int)std::min<int64_t>(std::max<int64_t>(env_i64("PINOT_AMD_GATE_DEPTH", 1), 1), 4);
     }
     L.jit = jit_get(jp, &r->jit_status);
@@ -4001,10 +4051,10 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // little per doc and is bound by those reservations: 4 per CU (swept 1/2/4/8: 1 % inverted
       // 1.42/1.31/1.27/1.38 ms); the tile-level select needs its occupancy (2 per CU: SSB Q1.2 0.65 -> 0.92 ms)
       if (jp.word_select) nb = std::min(nb, 4);
-      if (const char* e = getenv("PINOT_AMD_SELECT_PER_CU")) nb = std::max(1, std::min(nb, atoi(e)));
+      if (const char* e = knob("PINOT_AMD_SELECT_PER_CU")) nb = std::max(1, std::min(nb, atoi(e)));
       per_cu = nb;
       L.gather_grid = cus * ng;
-      if (const char* e = getenv("PINOT_AMD_GATHER_BLOCKS")) L.gather_grid = std::max(1, std::min(L.gather_grid, atoi(e)));
+      if (const char* e = knob("PINOT_AMD_GATHER_BLOCKS")) L.gather_grid = std::max(1, std::min(L.gather_grid, atoi(e)));
       for (size_t k = 0; k < L.segs.size(); ++k)
         for (int sl = 0; sl < nslots; ++sl) {
           const double bpr = slot_bpr(ls[k].cols[sl]);

@@ -1854,12 +1854,16 @@ hipError_t launch_pack_sel(const void* conts, const int32_t* sel, int64_t n, int
 // Swept on configs[2] (profiles/r03/sweep_inv_expand_group.txt): 4 beats 8 (a 64 KiB LDS bitset halves
 // the blocks per CU) and 1 (every small container its own line fetch)
 int expand_group() {
+#ifdef PINOT_AMD_DIAGNOSTICS  // the sweep's knob (diagnostics builds only)
   static const int g = [] {
     const char* e = getenv("PINOT_AMD_EXPAND_GROUP");
     const int v = e ? atoi(e) : 4;
     return v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }();
   return g;
+#else
+  return 4;
+#endif
 }
 
 hipError_t launch_roaring_select(const void* d_jobs, const void* d_fs, int32_t nfs, int64_t total_items, const void* d_segs,
