@@ -1,6 +1,6 @@
 # Knob sweeps on one box (env knobs of the planner), one bench line per setting:
-# (Experiment knobs outside host.cpp's knob() list are read only by a diagnostics build: python -m pinot_amd.build
-# with HIPCC flags adding -DPINOT_AMD_DIAGNOSTICS; the kept planner overrides work in every build.)
+# (Experiment knobs outside host.cpp's knob() list are read only by a diagnostics build: PINOT_AMD_BUILD_DIAGNOSTICS=1
+# python -m pinot_amd.build; the kept planner overrides work in every build.)
 #   SWEEP="PINOT_AMD_PREFETCH=2 PINOT_AMD_PREFETCH=8" ARGS="--workload ssb --query-index 11" bash scripts/gpu_sweep.sh
 set -o pipefail
 mkdir -p gpurun_out
