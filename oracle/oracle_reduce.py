@@ -164,23 +164,43 @@ def server_table(qc, groups: dict) -> dict:
 
 
 def segment_trim(qc, per_segment: list) -> dict:
-    """The segments' own trim, then the combine's merge of what they keep (GroupByOperator.java:157-175): a
-    segment holding more groups than trimSize keeps its top trimSize by the ORDER BY (TableResizer). Under a
-    safe trim -- ORDER BY expressions = GROUP BY expressions as sets, no HAVING (QueryContext.java:746-747) --
-    trimSize = LIMIT (QueryContext.calculateEffectiveSegmentGroupTrimSize, :568-580); otherwise no segment
-    trims here (minSegmentGroupTrimSize <= 0, the default: CommonConstants.java:1436). Groups outside the
-    global top LIMIT can thus carry partial results (only the segments whose top LIMIT they made).
+    """The segments' own trim, then the combine's merge of what they keep (GroupByOperator.java:152-172): a
+    segment holding more groups than trimSize keeps its top trimSize by the ORDER BY (TableResizer), trimSize from
+    QueryContext.calculateEffectiveSegmentGroupTrimSize (QueryContext.java:568-580):
+    * a safe trim -- ORDER BY expressions = GROUP BY expressions as sets, no HAVING (QueryContext.java:746-747) --
+      keeps LIMIT groups, ordered by the group values;
+    * an unsafe trim with minSegmentGroupTrimSize > 0 keeps max(5 * LIMIT, minSegmentGroupTrimSize) groups
+      (GroupByUtils.getTableCapacity, GroupByUtils.java:63-66), ordered by the ORDER BY on group values and final
+      aggregation values (extractFinalResult, Double.compare order); groups tied on every ORDER BY expression
+      in ascending group-key order (the order server_table breaks ties in: TableResizer's heap leaves them
+      unspecified, this restatement and the device both pin it);
+    * otherwise (minSegmentGroupTrimSize <= 0, the default: CommonConstants.java:1436) no segment trims.
+    Groups outside the global top LIMIT can thus carry partial results (only the segments whose top they made).
     per_segment: one {key: [partials]} dict per segment. Returns the combined {key: [partials]}."""
     targets = qc.order_by_targets() if qc.order_by else []
     safe = bool(targets) and all(kind == 0 for kind, _, _ in targets) and \
         sorted({idx for _, idx, _ in targets}) == list(range(len(qc.group_by)))
+    min_seg = getattr(qc, "min_segment_group_trim_size", -1)
+    if safe:
+        trim = qc.limit
+    elif targets and min_seg > 0:
+        trim = max(5 * qc.limit, min_seg)
+    else:
+        trim = -1
     out = {}
     for groups in per_segment:
         keep = list(groups)
-        if safe and qc.limit > 0 and len(groups) > qc.limit:
+        if trim > 0 and len(groups) > trim:
             def sk(k):
-                return tuple(_value_order(k[idx]) if asc else _Desc(_value_order(k[idx])) for _, idx, asc in targets)
-            keep = sorted(groups, key=sk)[:qc.limit]
+                parts = []
+                for kind, idx, asc in targets:
+                    if kind == 0:
+                        o = _value_order(k[idx])
+                    else:
+                        o = _final_order(final(qc.aggregations[idx].func, groups[k][idx]))
+                    parts.append(o if asc else _Desc(o))
+                return tuple(parts) + (tuple(_value_order(v) for v in reversed(k)),)
+            keep = sorted(groups, key=sk)[:trim]
         for k in keep:
             if k not in out:
                 out[k] = list(groups[k])

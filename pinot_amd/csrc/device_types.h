@@ -183,6 +183,22 @@ struct DevHash {
 };
 constexpr int kSpillMaxParts = 2048;  // spill partitions (the scan block's LDS histogram)
 
+// Segment-level group trim over a hash plan's (key, segment) scan table (GroupByOperator.java:157-175,
+// TableResizer.trimInSegmentResults): each segment keeps its top `keep` groups in the ORDER BY's order. The order is
+// a chain of 64-bit stage keys compared lexicographically, smaller first: kind 0 = ORDER BY group columns (merged ids
+// from the packed key words, DESC ones flipped, packed into one mixed-radix value while it fits), kind 1 = an
+// ORDER BY aggregation's final value (extractFinalResult, Double.compare order, DESC complemented), kind 2 = a key
+// word (ties in ascending group key, the last word first). Found per segment by a radix select, 8 bits per pass.
+struct SegSelStage {
+  int32_t kind;
+  int32_t ncols;  // kind 0
+  int32_t word[kMaxGroupCols], shift[kMaxGroupCols], bits[kMaxGroupCols], flip[kMaxGroupCols];
+  int64_t size[kMaxGroupCols], mul[kMaxGroupCols];
+  int32_t agg_type, acc, acc2, desc;  // kind 1: pinot_amd_agg_type, its accumulator (and MINMAXRANGE's max)
+  int32_t kword;                      // kind 2
+};
+constexpr int kSegSelMaxStages = 16;
+
 // Group keys by value for the cross-rank merge (the broker reduce on the device): group column j's
 // merged id sits in bits [shift[j], shift[j] + bits) of key word word[j] (the hash plan's packing, <= 63
 // bits per word); a dense table's key decomposes as id_j = (key / stride[j]) % size[j] (mixed radix).

@@ -42,7 +42,13 @@ hipError_t launch_trim(const unsigned long long* keys, int64_t cap, int nw_seg, 
                        int64_t* dstar, unsigned long long* limit_reached, hipStream_t st);
 hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int nw, int has_seg, const uint64_t* sacc,
                              unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q, int fd_acc,
-                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st);
+                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st,
+                             const SegSelStage* sst = nullptr, int nst = 0, const int32_t* sdone = nullptr,
+                             const uint64_t* scut = nullptr);
+hipError_t launch_segsel(const unsigned long long* keys, int64_t cap, int nw, const uint64_t* acc, int fd_acc,
+                         const int64_t* dstar, const DevQuery& q, const SegSelStage* sst, int nst, int32_t nsegs,
+                         int64_t keep, unsigned long long* cnt, int64_t* want, int32_t* done, uint64_t* prefix,
+                         uint64_t* cut, uint32_t* hist, hipStream_t st);
 hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const unsigned long long* seen_n, int64_t cap,
                         int32_t nsegs, int64_t limit, const int64_t* bucket_base, int64_t max_buckets, uint32_t* hist,
                         int64_t* bstar, int64_t* rank, unsigned long long* bitmap, int64_t* dstar,
@@ -1459,6 +1465,13 @@ struct pinot_amd_result {
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
   bool check_failed = false;  // the last execution's partitioned self-check failed (verify_partitioned)
+  // segment-level group trim over the (key, segment) scan table of a hash plan (SegSelStage, launch_segsel): the
+  // safe trim past the dense cap (keep = LIMIT) and the unsafe trim with minSegmentGroupTrimSize (keep =
+  // max(minSegmentGroupTrimSize, 5 x LIMIT)), each segment's top `keep` groups in the ORDER BY's order
+  bool segsel = false;
+  int64_t segsel_keep = 0;
+  std::vector<SegSelStage> segsel_st;
+  DevBuf d_segsel_st, ss_cnt, ss_want, ss_done, ss_prefix, ss_cut, ss_hist;
   std::string check_msg;
   DevBuf part_hw;  // per launch: the count and scatter blocks' placement and tallies (DevPartition::hw)
   DevBuf eff_begin, ovf_n, ovf_rec, ovf_part;  // sampled plans: allotment prefix, overflow slab
@@ -2465,8 +2478,18 @@ static int run_plan(pinot_amd_result* r) {
         HIP_OK(launch_trim(H.keys, H.cap, r->nw + 1, table, r->fd_acc, nb, r->limit, bb, (uint32_t*)r->t_hist.p,
                            (unsigned long long*)r->t_distinct.p, (int64_t*)r->t_bstar.p, (int64_t*)r->t_rank.p,
                            (unsigned long long*)r->t_bitmap.p, (int64_t*)r->t_dstar.p, limit_flag, st));
+        const SegSelStage* sst = nullptr;
+        const int nst = (int)r->segsel_st.size();
+        if (r->segsel) {  // each segment's top segsel_keep entries among the numGroupsLimit survivors
+          sst = (const SegSelStage*)r->d_segsel_st.p;
+          HIP_OK(launch_segsel(H.keys, H.cap, r->nw, table, r->fd_acc, (const int64_t*)r->t_dstar.p, r->q, sst, nst, nb,
+                               r->segsel_keep, (unsigned long long*)r->ss_cnt.p, (int64_t*)r->ss_want.p,
+                               (int32_t*)r->ss_done.p, (uint64_t*)r->ss_prefix.p, (uint64_t*)r->ss_cut.p,
+                               (uint32_t*)r->ss_hist.p, st));
+        }
         HIP_OK(launch_hash_merge(H.keys, H.cap, r->nw, 1, table, (unsigned long long*)r->fkeys.p, r->fcap,
-                                 (uint64_t*)r->acc.p, r->q, r->fd_acc, (const int64_t*)r->t_dstar.p, overflow, st));
+                                 (uint64_t*)r->acc.p, r->q, r->fd_acc, (const int64_t*)r->t_dstar.p, overflow, st, sst, nst,
+                                 (const int32_t*)r->ss_done.p, (const uint64_t*)r->ss_cut.p));
       }
     }
     if (r->trim) break;
@@ -2864,9 +2887,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
                                           "LIMIT %lld >= sortAggregateLimitThreshold %lld) disabled by PINOT_AMD_SEG_TRIM=0",
                   (long long)r->srv_limit, (long long)r->srv_sort_threshold);
   }
-  // Unsafe trim (ORDER BY other than the GROUP BY keys) with minSegmentGroupTrimSize > 0: each segment would keep
-  // its top max(minSegmentGroupTrimSize, 5 x LIMIT) groups by the ORDER BY, aggregation values included
-  // (QueryContext.java:575-578, GroupByOperator.java:157-175) -- not restated: refused when it would cut.
+  // Unsafe trim (ORDER BY other than the GROUP BY keys) with minSegmentGroupTrimSize > 0: each segment keeps its top
+  // max(minSegmentGroupTrimSize, 5 x LIMIT) groups by the ORDER BY, aggregation values included (QueryContext.java:
+  // 575-578, GroupByUtils.getTableCapacity, GroupByOperator.java:157-175): the (key, segment) hash plan with the
+  // per-segment selection (segsel) when some segment could hold more.
+  bool segsel_unsafe = false;
+  int64_t segsel_unsafe_keep = 0;
   if (!r->srv_safe && !r->srv_order.empty() && Q.min_seg_trim > 0 && r->srv_limit >= 0 && !filter_only &&
       !Q.group_by.empty()) {
     const int64_t seg_keep = std::max<int64_t>(Q.min_seg_trim, 5 * r->srv_limit);
@@ -2877,10 +2903,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       over = false;
       for (int si = 0; si < n; ++si) over |= std::min(seg_bound[si], seg_matched[si]) > seg_keep;
     }
-    if (over)
-      return fail(PINOT_AMD_EUNSUPPORTED, "segment group trim: minSegmentGroupTrimSize %lld with an ORDER BY other than the "
-                                          "GROUP BY keys would trim segments to %lld groups (not restated)",
-                  (long long)Q.min_seg_trim, (long long)seg_keep);
+    segsel_unsafe = over;
+    segsel_unsafe_keep = seg_keep;
   }
   // admission prefixes (dense trimming): the docs of segment si that should hold numGroupsLimit distinct
   // keys, twice the coupon-collector expectation for K uniform keys (K ln(K / (K - L)) matching docs,
@@ -3007,13 +3031,20 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   } else {
     r->kind = PLAN_DENSE;
   }
+  // segment-level trims the dense presence pass cannot restate: the safe trim past the dense cap and the unsafe
+  // trim (which orders by per-segment aggregation values): per-segment results in a (key, segment) scan table, the
+  // numGroupsLimit cutoff as for any trim plan, then each segment's top `keep` (segsel)
+  if ((seg_trim && r->kind != PLAN_DENSE) || segsel_unsafe) {
+    r->segsel = true;
+    r->segsel_keep = segsel_unsafe ? segsel_unsafe_keep : r->srv_limit;
+    seg_trim = false;
+    r->kind = PLAN_HASH;
+    r->trim = true;
+    r->admit = false;
+  }
   if (r->admit) admit_prefixes();
   std::vector<JitPlan::OrdCol> seg_ord;
   if (seg_trim) {
-    if (r->kind != PLAN_DENSE)
-      return fail(PINOT_AMD_EUNSUPPORTED, "server result limit: a segment-level safe trim (LIMIT %lld >= "
-                                          "sortAggregateLimitThreshold %lld) over a key space beyond the dense cap",
-                  (long long)r->srv_limit, (long long)r->srv_sort_threshold);
     // ORDER BY rank of a dense key: the first ORDER BY column most significant, DESC columns flipped
     std::vector<std::pair<int, int>> ocols;  // (group column, ascending), first occurrence of each column
     for (const auto& ob : r->srv_order)
@@ -3052,6 +3083,62 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     r->nw = r->pack_word.empty() ? 1 : r->pack_word.back() + 1;
     if (r->nw + (r->trim ? 1 : 0) > kMaxKeyWords)
       return fail(PINOT_AMD_EUNSUPPORTED, "group key of %d words exceeds %d", r->nw, kMaxKeyWords);
+    if (r->segsel) {
+      // the ORDER BY as a chain of 64-bit stage keys (SegSelStage): runs of group columns in one mixed-radix value
+      // while it fits (the first column most significant, DESC ones flipped), an aggregation's final value per
+      // stage, then -- unsafe trims, whose ORDER BY may tie -- the key words, the last first (ascending key)
+      auto& st = r->segsel_st;
+      st.clear();
+      SegSelStage cur{};
+      bool open = false;
+      unsigned __int128 span = 1;
+      auto close = [&]() {
+        if (open) st.push_back(cur);
+        open = false;
+      };
+      for (const auto& ob : r->srv_order) {
+        if (ob.kind == 0) {
+          const int j = ob.index;
+          const int64_t size = (int64_t)std::max<size_t>(r->keys[j]->size(), 1);
+          if (open && (span * (unsigned __int128)size > ((unsigned __int128)1 << 64) || cur.ncols >= kMaxGroupCols)) close();
+          if (!open) {
+            cur = SegSelStage{};
+            cur.kind = 0;
+            open = true;
+            span = 1;
+          }
+          for (int c = 0; c < cur.ncols; ++c) cur.mul[c] *= size;
+          const int c = cur.ncols++;
+          cur.word[c] = r->pack_word[j];
+          cur.shift[c] = r->pack_shift[j];
+          cur.bits[c] = r->pack_bits[j];
+          cur.flip[c] = ob.asc ? 0 : 1;
+          cur.size[c] = size;
+          cur.mul[c] = 1;
+          span *= (unsigned __int128)size;
+        } else {
+          close();
+          SegSelStage a{};
+          a.kind = 1;
+          a.agg_type = r->agg_type[ob.index];
+          a.acc = r->agg_acc[ob.index];
+          a.acc2 = r->agg_acc2[ob.index];
+          a.desc = ob.asc ? 0 : 1;
+          st.push_back(a);
+        }
+      }
+      close();
+      if (!r->srv_safe)
+        for (int w = r->nw - 1; w >= 0; --w) {
+          SegSelStage k{};
+          k.kind = 2;
+          k.kword = w;
+          st.push_back(k);
+        }
+      if (st.empty() || (int)st.size() > kSegSelMaxStages)
+        return fail(PINOT_AMD_EUNSUPPORTED, "segment group trim: %zu ORDER BY stages (at most %d)", st.size(), kSegSelMaxStages);
+      if (int rc = r->d_segsel_st.alloc_copy(st.data(), st.size() * sizeof(SegSelStage), 0)) return rc;
+    }
     const double keyspace = dense_keys;
     double fbound = 0;
     for (int si = 0; si < n; ++si) fbound += (double)(r->trim ? std::min<int64_t>(seg_bound[si], Q.num_groups_limit) : seg_bound[si]);
@@ -4211,6 +4298,15 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       if (int rc = r->t_rank.alloc((size_t)maxnb * 8)) return rc;
       if (int rc = r->t_dstar.alloc((size_t)maxnb * 8)) return rc;
       if (int rc = r->t_bitmap.alloc((size_t)maxnb * 16 * 8)) return rc;
+      if (r->segsel) {
+        const size_t E = r->segsel_st.size();
+        if (int rc = r->ss_cnt.alloc((size_t)maxnb * 8)) return rc;
+        if (int rc = r->ss_want.alloc((size_t)maxnb * 8)) return rc;
+        if (int rc = r->ss_done.alloc((size_t)maxnb * 4)) return rc;
+        if (int rc = r->ss_prefix.alloc((size_t)maxnb * 8)) return rc;
+        if (int rc = r->ss_cut.alloc((size_t)maxnb * E * 8)) return rc;
+        if (int rc = r->ss_hist.alloc((size_t)maxnb * 256 * 4)) return rc;
+      }
     }
   } else {
     if (int rc = r->acc.alloc((size_t)std::max(q.nacc, 1) * (size_t)std::max<int64_t>(num_keys, 1) * 8)) return rc;

@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #include "device_types.h"
+#include "../../include/pinot_amd.h"
 
 namespace pamd {
 
@@ -307,17 +308,172 @@ __global__ void admit_bits_kernel(uint32_t* first, int64_t nk, const uint32_t* s
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Segment-level group trim over a hash plan's (key, segment) scan table (SegSelStage; GroupByOperator.java:
+// 157-175): per segment, the `keep` smallest entries in the chain of stage keys. Stage by stage, 8 bits per pass,
+// each segment's candidates (entries tied with the cutoff on every earlier stage) are histogrammed on the current
+// digit (segsel_hist) and the digit holding the wanted rank is picked (segsel_pick); a stage whose cutoff value
+// holds exactly the wanted count ends the segment's selection there (done = stage), else its ties go on.
+// ------------------------------------------------------------------------------------------------
+// exact (lo, hi) two's complement 128-bit integer -> double, rounded to nearest even (as the host's
+// (double)(__int128) in final_value)
+__device__ __forceinline__ double i128_to_double_rn(uint64_t lo, uint64_t hi) {
+  const bool neg = (int64_t)hi < 0;
+  if (neg) {
+    lo = ~lo + 1ull;
+    hi = ~hi + (lo == 0ull ? 1ull : 0ull);
+  }
+  if (hi == 0ull && lo < (1ull << 53)) {
+    const double d = (double)lo;
+    return neg ? -d : d;
+  }
+  int e;  // bit index of the leading one
+  uint64_t m, rest;
+  if (hi) {
+    const int lz = __clzll((long long)hi);
+    e = 127 - lz;
+    m = lz ? (hi << lz) | (lo >> (64 - lz)) : hi;
+    rest = lz ? lo << lz : lo;
+  } else {
+    const int lz = __clzll((long long)lo);
+    e = 63 - lz;
+    m = lo << lz;
+    rest = 0ull;
+  }
+  uint64_t mant = m >> 11;
+  const uint64_t r = m & 0x7FFull;
+  if (r > 0x400ull || (r == 0x400ull && (rest != 0ull || (mant & 1ull)))) mant += 1ull;
+  const double d = ldexp((double)mant, e - 52);
+  return neg ? -d : d;
+}
+__device__ __forceinline__ double decode_ordered_dev(uint64_t u, int op) {
+  if (op == ACC_MIN && u == ~0ull) return __builtin_inf();
+  if (op == ACC_MAX && u == 0ull) return -__builtin_inf();
+  const uint64_t b = (u >> 63) ? (u & 0x7FFFFFFFFFFFFFFFull) : ~u;
+  return __longlong_as_double((long long)b);
+}
+// Double.compare order as an unsigned key (every NaN one value above +inf, -0.0 below 0.0)
+__device__ __forceinline__ uint64_t java_double_key(double d) {
+  uint64_t b = d != d ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+// extractFinalResult of a SegSelStage's aggregation from scan-table slot i (host.cpp final_value)
+__device__ double segsel_final(const SegSelStage& g, const DevQuery& q, const uint64_t* acc, int64_t cap, int64_t i) {
+  auto A = [&](int a) { return acc[(uint64_t)a * (uint64_t)cap + (uint64_t)i]; };
+  const int op = q.acc_op[g.acc];
+  const uint64_t w = A(g.acc);
+  const uint64_t cnt = A(0);
+  auto sum = [&]() -> double {
+    if (op == ACC_SUM_F64) return u64_as_double(w);
+    if (op == ACC_SUM_I128) return i128_to_double_rn(w, A(g.acc + 1));
+    return i128_to_double_rn(w, (int64_t)w < 0 ? ~0ull : 0ull);
+  };
+  switch (g.agg_type) {
+    case PINOT_AMD_AGG_COUNT: return (double)cnt;
+    case PINOT_AMD_AGG_AVG: return cnt ? sum() / (double)cnt : -__builtin_inf();
+    case PINOT_AMD_AGG_MIN:
+    case PINOT_AMD_AGG_MAX: return decode_ordered_dev(w, op);
+    case PINOT_AMD_AGG_MINMAXRANGE: return decode_ordered_dev(A(g.acc2), ACC_MAX) - decode_ordered_dev(w, ACC_MIN);
+    default: return sum();
+  }
+}
+__device__ uint64_t segsel_key(const SegSelStage& g, const DevQuery& q, const unsigned long long* keys,
+                               const uint64_t* acc, int64_t cap, int64_t i) {
+  if (g.kind == 2) return keys[(uint64_t)g.kword * (uint64_t)cap + (uint64_t)i];
+  if (g.kind == 1) {
+    const uint64_t k = java_double_key(segsel_final(g, q, acc, cap, i));
+    return g.desc ? ~k : k;
+  }
+  uint64_t u = 0ull;
+  for (int c = 0; c < g.ncols; ++c) {
+    const uint64_t w = keys[(uint64_t)g.word[c] * (uint64_t)cap + (uint64_t)i];
+    uint64_t id = (w >> g.shift[c]) & (g.bits[c] >= 64 ? ~0ull : ((1ull << g.bits[c]) - 1ull));
+    if (g.flip[c]) id = (uint64_t)g.size[c] - 1ull - id;
+    u += id * (uint64_t)g.mul[c];
+  }
+  return u;
+}
+// a present entry of the scan table that the numGroupsLimit cutoff admitted; its segment (batch index)
+__device__ __forceinline__ bool segsel_entry(const unsigned long long* keys, int64_t cap, int nw, const uint64_t* acc,
+                                             int fd_acc, const int64_t* dstar, int64_t i, int64_t* s) {
+  if (acc[i] == 0ull) return false;
+  *s = (int64_t)keys[(uint64_t)nw * (uint64_t)cap + (uint64_t)i];
+  return !dstar || acc[(uint64_t)fd_acc * (uint64_t)cap + (uint64_t)i] <= (uint64_t)dstar[*s];
+}
+// entry i against its segment's cutoffs on stages [0, upto): -1 below, 0 tied on all, 1 above
+__device__ __forceinline__ int segsel_cmp(const SegSelStage* st, const DevQuery& q, const unsigned long long* keys,
+                                          const uint64_t* acc, int64_t cap, int64_t i, const uint64_t* cut, int upto) {
+  for (int j = 0; j < upto; ++j) {
+    const uint64_t u = segsel_key(st[j], q, keys, acc, cap, i);
+    if (u != cut[j]) return u < cut[j] ? -1 : 1;
+  }
+  return 0;
+}
+
+__global__ void segsel_count_kernel(const unsigned long long* keys, int64_t cap, int nw, const uint64_t* acc, int fd_acc,
+                                    const int64_t* dstar, unsigned long long* cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s;
+    if (segsel_entry(keys, cap, nw, acc, fd_acc, dstar, i, &s)) atomicAdd(&cnt[s], 1ull);
+  }
+}
+// want[s] = keep; done[s] = -2 when the segment holds <= keep candidates (nothing trimmed), else -1 (selecting)
+__global__ void segsel_init_kernel(int32_t nsegs, int64_t keep, const unsigned long long* cnt, int64_t* want, int32_t* done,
+                                   uint64_t* prefix) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs) return;
+  want[s] = keep;
+  done[s] = (int64_t)cnt[s] <= keep ? -2 : -1;
+  prefix[s] = 0ull;
+}
+__global__ void segsel_hist_kernel(const unsigned long long* keys, int64_t cap, int nw, const uint64_t* acc, int fd_acc,
+                                   const int64_t* dstar, DevQuery q, const SegSelStage* st, int nst, int j, int d,
+                                   const int32_t* done, const uint64_t* prefix, const uint64_t* cut, uint32_t* hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s;
+    if (!segsel_entry(keys, cap, nw, acc, fd_acc, dstar, i, &s) || done[s] != -1) continue;
+    if (j > 0 && segsel_cmp(st, q, keys, acc, cap, i, cut + s * nst, j) != 0) continue;
+    const uint64_t u = segsel_key(st[j], q, keys, acc, cap, i);
+    if (d < 7 && (u >> (8 * (d + 1))) != (prefix[s] >> (8 * (d + 1)))) continue;
+    atomicAdd(&hist[s * 256 + (int64_t)((u >> (8 * d)) & 255ull)], 1u);
+  }
+}
+__global__ void segsel_pick_kernel(int32_t nsegs, int nst, int j, int d, const uint32_t* hist, int64_t* want, int32_t* done,
+                                   uint64_t* prefix, uint64_t* cut) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsegs || done[s] != -1) return;
+  int64_t cum = 0;
+  for (int b = 0; b < 256; ++b) {
+    const int64_t h = hist[(int64_t)s * 256 + b];
+    if (cum + h < want[s]) {
+      cum += h;
+      continue;
+    }
+    prefix[s] |= (uint64_t)b << (8 * d);
+    want[s] -= cum;
+    if (d == 0) {  // the stage's cutoff value; h candidates hold it exactly
+      cut[(int64_t)s * nst + j] = prefix[s];
+      prefix[s] = 0ull;
+      if (h == want[s] || j + 1 >= nst) done[s] = j;
+    }
+    return;
+  }
+}
+
 // Fold a scan table into the final table: every present entry (admitted by the trim cutoff when
 // dstar != nullptr; the segment word is dropped from the key) is inserted by key and its
 // accumulators applied with the plan's ops (AggregationFunction.merge of the combine).
 __global__ void hash_merge_kernel(const unsigned long long* skeys, int64_t scap, int nw, int has_seg,
                                   const uint64_t* sacc, unsigned long long* fkeys, int64_t fcap, uint64_t* facc,
-                                  DevQuery q, int fd_acc, const int64_t* dstar, unsigned long long* overflow) {
+                                  DevQuery q, int fd_acc, const int64_t* dstar, unsigned long long* overflow,
+                                  const SegSelStage* st, int nst, const int32_t* sdone, const uint64_t* scut) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < scap; i += (int64_t)gridDim.x * blockDim.x) {
     if (sacc[i] == 0ull) continue;
     if (dstar) {
       const int64_t s = (int64_t)skeys[(uint64_t)nw * (uint64_t)scap + i];
       if (sacc[(uint64_t)fd_acc * (uint64_t)scap + i] > (uint64_t)dstar[s]) continue;
+      // segment-level trim: only the segment's top entries (lexicographically <= its cutoffs up to its last stage)
+      if (st && sdone[s] >= 0 && segsel_cmp(st, q, skeys, sacc, scap, i, scut + s * nst, sdone[s] + 1) > 0) continue;
     }
     uint64_t kw[kMaxKeyWords];
     for (int w = 0; w < nw; ++w) kw[w] = skeys[(uint64_t)w * (uint64_t)scap + i];
@@ -1696,9 +1852,33 @@ hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const
 
 hipError_t launch_hash_merge(const unsigned long long* skeys, int64_t scap, int nw, int has_seg, const uint64_t* sacc,
                              unsigned long long* fkeys, int64_t fcap, uint64_t* facc, const DevQuery& q, int fd_acc,
-                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st) {
+                             const int64_t* dstar, unsigned long long* overflow, hipStream_t st, const SegSelStage* sst,
+                             int nst, const int32_t* sdone, const uint64_t* scut) {
   hipLaunchKernelGGL(hash_merge_kernel, dim3(grid_cap(scap, kBlock, 8192)), dim3(kBlock), 0, st, skeys, scap, nw, has_seg,
-                     sacc, fkeys, fcap, facc, q, fd_acc, dstar, overflow);
+                     sacc, fkeys, fcap, facc, q, fd_acc, dstar, overflow, sst, nst, sdone, scut);
+  return hipGetLastError();
+}
+
+// the segment-level trim's selection over one trim batch's scan table (after launch_trim: dstar admits the
+// numGroupsLimit survivors): per segment `keep` entries, cutoffs per stage in cut (nsegs x nst), done per segment
+// (-2: nothing trimmed; j: selection ended at stage j). hist: nsegs x 256 words, zeroed per pass here.
+hipError_t launch_segsel(const unsigned long long* keys, int64_t cap, int nw, const uint64_t* acc, int fd_acc,
+                         const int64_t* dstar, const DevQuery& q, const SegSelStage* sst, int nst, int32_t nsegs,
+                         int64_t keep, unsigned long long* cnt, int64_t* want, int32_t* done, uint64_t* prefix,
+                         uint64_t* cut, uint32_t* hist, hipStream_t st) {
+  if (nsegs <= 0 || nst <= 0) return hipSuccess;
+  const unsigned g = grid_cap(cap, kBlock, 8192), gs = grid_for(nsegs, kBlock);
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)nsegs * 8, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(segsel_count_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw, acc, fd_acc, dstar, cnt);
+  hipLaunchKernelGGL(segsel_init_kernel, dim3(gs), dim3(kBlock), 0, st, nsegs, keep, cnt, want, done, prefix);
+  for (int j = 0; j < nst; ++j)
+    for (int d = 7; d >= 0; --d) {
+      if ((e = hipMemsetAsync(hist, 0, (size_t)nsegs * 256 * 4, st)) != hipSuccess) return e;
+      hipLaunchKernelGGL(segsel_hist_kernel, dim3(g), dim3(kBlock), 0, st, keys, cap, nw, acc, fd_acc, dstar, q, sst, nst, j,
+                         d, done, prefix, cut, hist);
+      hipLaunchKernelGGL(segsel_pick_kernel, dim3(gs), dim3(kBlock), 0, st, nsegs, nst, j, d, hist, want, done, prefix, cut);
+    }
   return hipGetLastError();
 }
 

@@ -122,39 +122,97 @@ def test_segment_level_safe_trim_untrimmed_segments():
     assert got == server_table(oracle.parse_sql(q2), full)
 
 
-def test_unsafe_segment_trim_option_refused():
-    """minSegmentGroupTrimSize > 0 with an ORDER BY on an aggregation (an unsafe trim): each segment would keep its
-    top max(value, 5 x LIMIT) groups by aggregation values (QueryContext.java:575-578) -- not restated, refused when
-    a segment could hold more; with few enough groups per segment it cuts nothing and is accepted."""
+UNSAFE_TRIM_QUERIES = [
+    # unsafe trim (an ORDER BY other than the GROUP BY keys) with minSegmentGroupTrimSize > 0: each segment keeps its
+    # top max(minSegmentGroupTrimSize, 5 x LIMIT) groups by the ORDER BY on final values (QueryContext.java:568-580)
+    "SET minSegmentGroupTrimSize = 10; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY COUNT(*) DESC LIMIT 2",
+    "SET minSegmentGroupTrimSize = 40; SET minServerGroupTrimSize = 60; SELECT d0, d1, SUM(r_long), AVG(r_int) FROM t "
+    "GROUP BY d0, d1 ORDER BY SUM(r_long) DESC LIMIT 3",
+    "SET minSegmentGroupTrimSize = 5; SELECT d0, AVG(r_int), MAX(r_double) FROM t WHERE r_int > 0 GROUP BY d0 "
+    "ORDER BY AVG(r_int) LIMIT 6",
+    "SET minSegmentGroupTrimSize = 25; SELECT d1, d0, MIN(r_double), COUNT(*) FROM t GROUP BY d1, d0 "
+    "ORDER BY d1 DESC, MIN(r_double) LIMIT 4",
+    "SET minSegmentGroupTrimSize = 30; SELECT d0, MINMAXRANGE(r_int), SUMLONG(r_long) FROM t GROUP BY d0 "
+    "ORDER BY MINMAXRANGE(r_int) DESC, SUMLONG(r_long) LIMIT 5",
+    # after numGroupsLimit admission (each segment's first 500 groups, then its top 50 by COUNT)
+    "SET numGroupsLimit = 500; SET minSegmentGroupTrimSize = 50; SELECT d0, d1, COUNT(*), SUM(r_long) FROM t "
+    "GROUP BY d0, d1 ORDER BY COUNT(*) DESC, SUM(r_long) LIMIT 3",
+]
+
+
+@pytest.mark.parametrize("plan", ["auto", "hash"])
+@pytest.mark.parametrize("qi", range(len(UNSAFE_TRIM_QUERIES)))
+def test_unsafe_segment_trim_vs_oracle(qi, plan, monkeypatch):
+    """The unsafe segment trim on the device (the (key, segment) hash plan, then per segment a radix selection of
+    its top entries over the ORDER BY's stage keys -- group ids, final aggregation values in Double.compare order,
+    the key words for ties) against oracle_reduce.segment_trim then server_table. Ties on every ORDER BY
+    expression go in ascending group-key order on both sides (TableResizer's heap leaves them unspecified)."""
     import torch
     assert torch.cuda.is_available()
-    from pinot_amd import _lib
+    from oracle_reduce import segment_trim
+    from pinot_amd import engine as E
+    if plan == "hash":
+        monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    rng = np.random.default_rng(130 + qi)
+    bufs = [random_segment(rng, 20_000 + 2_000 * i, name=f"su{i}", bits_cards=(300, 37)) for i in range(3)]
+    segs = [E.ImmutableSegment(b) for b in bufs]
+    q = UNSAFE_TRIM_QUERIES[qi]
+    qc = parse_sql(q)
+    got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
+    oq = oracle.parse_sql(q)
+    per_seg = [oracle.execute(q, [b])[1] for b in bufs]
+    keep = max(5 * qc.limit, oq.min_segment_group_trim_size)
+    assert max(len(g) for g in per_seg) > keep  # some segment trims
+    trimmed = segment_trim(oq, per_seg)
+    exp = server_table(oq, trimmed)
+    _, full = oracle.execute(q, bufs)
+    assert trimmed != full  # the segment trim drops or cuts groups
+    assert len(got) == len(exp)
+    assert_same_groups(got, exp, set())
+    assert list(got) == list(exp)
+
+
+def test_unsafe_segment_trim_untrimmed_segments():
+    """minSegmentGroupTrimSize above every segment's group count: nothing to trim (the plan keeps its kind)."""
+    import torch
+    assert torch.cuda.is_available()
     from pinot_amd import engine as E
     rng = np.random.default_rng(9)
     bufs = [random_segment(rng, 20_000, name="su0", bits_cards=(300, 37))]
     segs = [E.ImmutableSegment(b) for b in bufs]
-    q = "SET minSegmentGroupTrimSize = 10; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY COUNT(*) DESC LIMIT 2"
-    with pytest.raises(_lib.PinotAmdError, match="minSegmentGroupTrimSize"):
-        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
     q2 = "SET minSegmentGroupTrimSize = 1000; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY COUNT(*) DESC LIMIT 2"
     got = E.ServerQueryExecutor(server_trim=True).execute(q2, segs).groups()
     _, full = oracle.execute(q2, bufs)
     assert list(got) == list(server_table(oracle.parse_sql(q2), full))
 
 
-def test_segment_level_safe_trim_hash_plan_refused(monkeypatch):
-    """A hash-table plan (key space past the dense cap) does not restate the segment-level trim: refused."""
+@pytest.mark.parametrize("plan", ["hash", "cap"])
+@pytest.mark.parametrize("qi", range(len(SEG_TRIM_QUERIES)))
+def test_segment_level_safe_trim_hash_plan_vs_oracle(qi, plan, monkeypatch):
+    """The segment-level safe trim over a hash plan's key space (forced, or a key space past the dense cap): the
+    (key, segment) scan table, each segment's top LIMIT entries by the ORDER BY's group ids (segsel), against the
+    oracle's segment_trim then server_table."""
     import torch
     assert torch.cuda.is_available()
-    from pinot_amd import _lib
+    from oracle_reduce import segment_trim
     from pinot_amd import engine as E
-    monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
-    rng = np.random.default_rng(8)
-    bufs = [random_segment(rng, 20_000, name="sh0", bits_cards=(300, 37))]
+    if plan == "hash":
+        monkeypatch.setenv("PINOT_AMD_GROUP_PLAN", "hash")
+    else:
+        monkeypatch.setenv("PINOT_AMD_DENSE_MAX_KEYS", "64")
+    rng = np.random.default_rng(90 + qi)
+    bufs = [random_segment(rng, 25_000 + 3_000 * i, name=f"sg{i}", bits_cards=(300, 37)) for i in range(3)]
     segs = [E.ImmutableSegment(b) for b in bufs]
-    q = "SET sortAggregateLimitThreshold = 5; SELECT d0, COUNT(*) FROM t GROUP BY d0 ORDER BY d0 LIMIT 5"
-    with pytest.raises(_lib.PinotAmdError, match="segment-level safe trim"):
-        E.ServerQueryExecutor(server_trim=True).execute(q, segs).groups()
+    q = SEG_TRIM_QUERIES[qi]
+    qc = parse_sql(q)
+    got = E.ServerQueryExecutor(server_trim=True).execute(qc, segs).groups()
+    oq = oracle.parse_sql(q)
+    per_seg = [oracle.execute(q, [b])[1] for b in bufs]
+    assert max(len(g) for g in per_seg) > qc.limit
+    exp = server_table(oq, segment_trim(oq, per_seg))
+    assert len(got) == len(exp)
+    assert_same_groups(got, exp, set())
+    assert list(got) == list(exp)
 
 
 def test_ssb_server_table_vs_oracle():
