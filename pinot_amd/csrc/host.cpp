@@ -130,8 +130,7 @@ namespace {
 // Runtime knobs. A default build reads only the planner overrides the test suite exercises and the server's resource
 // limits (the list below); the experiment knobs of earlier rounds' sweeps (DESIGN.md records their outcomes) are
 // honoured only in a diagnostics build (-DPINOT_AMD_DIAGNOSTICS), so a default build plans from the query alone.
-static const char* knob(const char* name) {
-#ifndef PINOT_AMD_DIAGNOSTICS
+static const std::set<std::string>& kept_knobs() {
   static const std::set<std::string> kept = {
       "PINOT_AMD_ADMIT_PREFIX",
       "PINOT_AMD_ADMIT_SEQ",
@@ -171,10 +170,28 @@ static const char* knob(const char* name) {
       "PINOT_AMD_HASH_FINAL_MAX_BYTES",
       "PINOT_AMD_ADMIT_MAX_BYTES",
       "PINOT_AMD_DENSE_MAX_KEYS",
+      "PINOT_AMD_PLAN_CACHE",
+      "PINOT_AMD_PLAN_CACHE_BYTES",
   };
-  if (!kept.count(name)) return nullptr;
+  return kept;
+}
+static const char* knob(const char* name) {
+#ifndef PINOT_AMD_DIAGNOSTICS
+  if (!kept_knobs().count(name)) return nullptr;
 #endif
   return getenv(name);
+}
+// every knob a default build reads, with its value: part of a prepared plan's identity (a plan built under other
+// overrides is another plan); empty in a diagnostics build, whose knobs are open-ended (no plan cache there)
+static std::string knob_snapshot() {
+#ifdef PINOT_AMD_DIAGNOSTICS
+  return std::string();
+#else
+  std::string out = "knobs";
+  for (const std::string& k : kept_knobs())
+    if (const char* v = getenv(k.c_str())) out += "|" + k + "=" + v;
+  return out;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -244,6 +261,7 @@ static DevPool& dev_pool() {
 }
 // set by pinot_amd_result_destroy while the result's members are destroyed (its stream synchronised)
 static thread_local bool g_release_to_pool = false;
+static thread_local size_t g_tl_alloc_bytes = 0;  // device bytes this thread allocated (a plan's footprint)
 
 struct DevBuf {
   void* p = nullptr;
@@ -263,6 +281,7 @@ struct DevBuf {
     n = len;
     const size_t want = len ? len : 1;
     bsz = DevPool::block_size(want);
+    g_tl_alloc_bytes += bsz <= DevPool::kPoolMaxBlock ? bsz : want;
     if (bsz <= DevPool::kPoolMaxBlock) {
       if ((p = dev_pool().take(bsz))) return 0;
       if (hipMalloc(&p, bsz) == hipSuccess) return 0;
@@ -846,6 +865,22 @@ static int stage_compressed_chunks(Column& c, const pinot_amd_column_spec* spec,
   return 0;
 }
 
+// segments alive (created, not destroyed): a prepared plan goes back to the plan cache only while every segment it
+// reads is alive
+static std::mutex g_live_mu;
+static std::set<uint64_t> g_live_uids;
+static void note_segment_live(uint64_t uid, bool live) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (live) g_live_uids.insert(uid);
+  else g_live_uids.erase(uid);
+}
+static bool segments_live(const std::vector<uint64_t>& uids) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  for (uint64_t u : uids)
+    if (!g_live_uids.count(u)) return false;
+  return true;
+}
+
 extern "C" {
 
 int pinot_amd_abi_version(void) { return PINOT_AMD_ABI_VERSION; }
@@ -865,6 +900,7 @@ int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segme
   s->num_docs = num_docs;
   static std::atomic<uint64_t> next_uid{1};
   s->uid = next_uid.fetch_add(1);
+  note_segment_live(s->uid, true);
   *out = s;
   return 0;
 }
@@ -872,7 +908,8 @@ int pinot_amd_segment_create(const char* name, int64_t num_docs, pinot_amd_segme
 static void drop_segment_caches(uint64_t uid);
 
 int pinot_amd_segment_destroy(pinot_amd_segment* seg) {
-  if (seg) drop_segment_caches(seg->uid);  // merged key spaces and remaps over it (host.cpp key caches)
+  if (seg) note_segment_live(seg->uid, false);
+  if (seg) drop_segment_caches(seg->uid);  // merged key spaces, remaps and prepared plans over it
   if (seg) {
     std::lock_guard<std::mutex> g(g_print_mu);
     for (auto& kv : seg->cols) g_prints.erase(kv.second->fwd.p);
@@ -1465,6 +1502,10 @@ struct pinot_amd_result {
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
   bool check_failed = false;  // the last execution's partitioned self-check failed (verify_partitioned)
+  // prepared-plan cache (plan_cache_*): the identity this plan was built for, the segments it reads, its device bytes
+  std::string plan_key;
+  std::vector<uint64_t> plan_uids;
+  size_t plan_bytes = 0;
   // segment-level group trim over the (key, segment) scan table of a hash plan (SegSelStage, launch_segsel): the
   // safe trim past the dense cap (keep = LIMIT) and the unsafe trim with minSegmentGroupTrimSize (keep =
   // max(minSegmentGroupTrimSize, 5 x LIMIT)), each segment's top `keep` groups in the ORDER BY's order
@@ -1553,6 +1594,136 @@ struct pinot_amd_result {
 };
 
 namespace {
+
+// ------------------------------------------------------------------------------------------------
+// Prepared-plan cache. A server re-issues the same query over the same segments (dashboards, retries, the
+// broker's per-server fan-out of a repeated query); a destroyed result's plan -- its generated kernels, device
+// descriptors, leaf tables, group tables, grown capacities -- is kept, idle, under the identity it was built
+// for, and the next execute of that identity takes it and only runs it (run_plan, the work execute_again does),
+// skipping the host planning (predicate leaves, key spaces, plan choice, descriptor packing, buffer setup).
+// Identity: the query (every field of pinot_amd_query, the installed key spaces by id), filter-only or not, the
+// segments by (uid, generation), the device, and the planner overrides in the environment. A plan reading a
+// destroyed segment is dropped with it (drop_segment_caches); a plan whose self-check failed is never kept.
+// At most PINOT_AMD_PLAN_CACHE_BYTES (default 2 GiB) of plan device memory, 64 plans, least recently used out
+// first; a plan above a quarter of the budget is freed as before. PINOT_AMD_PLAN_CACHE=0 disables the cache.
+// ------------------------------------------------------------------------------------------------
+struct PlanCacheEntry {
+  std::unique_ptr<pinot_amd_result> r;
+  uint64_t used = 0;
+};
+static std::mutex g_plan_mu;
+static std::multimap<std::string, PlanCacheEntry> g_plans;
+static size_t g_plan_bytes = 0;
+static uint64_t g_plan_clock = 0;
+
+static bool plan_cache_on() {
+  static const bool on = [] {
+    const char* v = knob("PINOT_AMD_PLAN_CACHE");
+    return !(v && std::string(v) == "0");
+  }();
+  return on;
+}
+static size_t plan_cache_budget() {
+  static const size_t b = [] {
+    const char* v = knob("PINOT_AMD_PLAN_CACHE_BYTES");
+    return v ? (size_t)std::max(0ll, atoll(v)) : (size_t)2 << 30;
+  }();
+  return b;
+}
+
+static std::string plan_identity(const pinot_amd_query& Q, const std::vector<pinot_amd_segment*>& segs, bool filter_only) {
+  const std::string ks = knob_snapshot();
+  if (ks.empty() || !plan_cache_on()) return std::string();
+  std::string k = filter_only ? "F|" : "Q|";
+  auto num = [&](long long v) { k += std::to_string(v) + ","; };
+  k += preds_signature(Q.preds) + "|G";
+  for (const std::string& g : Q.group_by) k += g + '\x1f';
+  k += "|K";
+  for (const auto& kv : Q.key_space) k += kv.first + "=" + std::to_string(kv.second ? kv.second->id : 0) + '\x1f';
+  k += "|A";
+  for (const AggSpec& a : Q.aggs) {
+    num(a.type);
+    k += a.column + '\x1f';
+    num(a.expr);
+    k += a.column2 + '\x1f';
+  }
+  k += "|O";
+  for (const auto& o : Q.order_by) {
+    num(o.kind);
+    num(o.index);
+    num(o.asc);
+  }
+  k += "|L";
+  for (long long v : {(long long)Q.num_groups_limit, (long long)Q.limit, (long long)Q.min_trim, (long long)Q.trim_threshold,
+                      (long long)Q.server_final, (long long)Q.sort_agg_threshold, (long long)Q.min_seg_trim})
+    num(v);
+  k += "|S";
+  for (auto* sg : segs) k += std::to_string(sg->uid) + "." + std::to_string(sg->gen) + ",";
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  k += "|D" + std::to_string(dev) + "|" + ks;
+  return k;
+}
+
+// an idle plan of this identity, or null
+static pinot_amd_result* plan_cache_take(const std::string& key) {
+  if (key.empty()) return nullptr;
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  auto it = g_plans.find(key);
+  if (it == g_plans.end()) return nullptr;
+  pinot_amd_result* r = it->second.r.release();
+  g_plan_bytes -= r->plan_bytes;
+  g_plans.erase(it);
+  return r;
+}
+
+// true: the cache keeps r (idle: its stream synchronised by the caller)
+static bool plan_cache_put(pinot_amd_result* r) {
+  if (r->plan_key.empty() || r->check_failed || !segments_live(r->plan_uids)) return false;
+  const size_t budget = plan_cache_budget();
+  if (r->plan_bytes > budget / 4) return false;
+  std::vector<std::unique_ptr<pinot_amd_result>> evicted;
+  {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    while (!g_plans.empty() && (g_plan_bytes + r->plan_bytes > budget || g_plans.size() >= 64)) {
+      auto lru = g_plans.begin();
+      for (auto it = g_plans.begin(); it != g_plans.end(); ++it)
+        if (it->second.used < lru->second.used) lru = it;
+      g_plan_bytes -= lru->second.r->plan_bytes;
+      evicted.push_back(std::move(lru->second.r));
+      g_plans.erase(lru);
+    }
+    PlanCacheEntry e;
+    e.r.reset(r);
+    e.used = ++g_plan_clock;
+    g_plan_bytes += r->plan_bytes;
+    g_plans.emplace(r->plan_key, std::move(e));
+  }
+  g_release_to_pool = true;  // evicted plans are idle: their blocks go to the device pool (outside the lock)
+  evicted.clear();
+  g_release_to_pool = false;
+  return true;
+}
+
+// plans reading segment uid (it is being destroyed)
+static void plan_cache_drop_uid(uint64_t uid) {
+  std::vector<std::unique_ptr<pinot_amd_result>> dropped;
+  {
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    for (auto it = g_plans.begin(); it != g_plans.end();) {
+      if (std::find(it->second.r->plan_uids.begin(), it->second.r->plan_uids.end(), uid) != it->second.r->plan_uids.end()) {
+        g_plan_bytes -= it->second.r->plan_bytes;
+        dropped.push_back(std::move(it->second.r));
+        it = g_plans.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  g_release_to_pool = true;  // idle plans (synchronised when cached)
+  dropped.clear();
+  g_release_to_pool = false;
+}
 
 // Dictionary.insertionIndexOf: index if found, else -(insertionPoint + 1)
 template <typename T, typename Less>
@@ -2026,6 +2197,7 @@ static size_t g_keys_bytes = 0;
 static uint64_t g_cache_clock = 0;
 
 static void drop_segment_caches(uint64_t uid) {
+  plan_cache_drop_uid(uid);
   std::lock_guard<std::mutex> g(g_keys_mu);
   for (auto it = g_keys_cache.begin(); it != g_keys_cache.end();) {
     if (std::find(it->second.uids.begin(), it->second.uids.end(), uid) != it->second.uids.end()) {
@@ -2630,9 +2802,23 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   std::vector<pinot_amd_segment*> segs(segs_in, segs_in + n);
   for (auto* s : segs)
     if (!s) return fail(PINOT_AMD_EINVAL, "execute: null segment");
+  const std::string plan_key = plan_identity(*qq, segs, filter_only);
+  if (pinot_amd_result* hit = plan_cache_take(plan_key)) {  // a prepared plan of this identity: run it
+    std::unique_ptr<pinot_amd_result> hold(hit);
+    hit->stream = (hipStream_t)stream;
+    PlanClock clk(&hit->plan_timing);
+    clk.mark("plan_cache");
+    if (int rc = run_plan(hit)) return rc;
+    clk.mark("launch");
+    *out = hold.release();
+    return 0;
+  }
+  const size_t alloc0 = g_tl_alloc_bytes;
   auto res = std::make_unique<pinot_amd_result>();
   pinot_amd_result* r = res.get();
   r->stream = (hipStream_t)stream;
+  r->plan_key = plan_key;
+  for (auto* sg : segs) r->plan_uids.push_back(sg->uid);
   PlanClock clk(&r->plan_timing);
   pinot_amd_query filter_q;
   if (filter_only) filter_q.preds = qq->preds;  // FilterPlanNode only: no projection, no aggregation
@@ -4362,6 +4548,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
   const bool cap_from_cache = r->cap_known;
   if (int rc = run_plan(r)) return rc;
   clk.mark("launch");
+  r->plan_bytes = g_tl_alloc_bytes - alloc0;
   if (r->kind == PLAN_HASH && !r->trim) {  // diagnostics: the table's slots, and whether an earlier execution sized it
     char b[96];
     snprintf(b, sizeof(b), ";hash_slots=%lld;hash_slots_remembered=%d", (long long)r->fcap, cap_from_cache ? 1 : 0);
@@ -4419,6 +4606,7 @@ int pinot_amd_result_destroy(pinot_amd_result* r) {
   // the result's work is finished before its blocks go to the device pool (a caller still reading a
   // pinot_amd_result_bitset buffer on another stream must order that read before this call)
   const bool idle = hipStreamSynchronize(r->stream) == hipSuccess;
+  if (idle && plan_cache_put(r)) return 0;  // kept for the next execute of its identity
   g_release_to_pool = idle;
   delete r;
   g_release_to_pool = false;

@@ -132,21 +132,39 @@ WIDE_COLUMNS = ("w1", "w2", "w3", "w4", "w5")
 _WIDE_MUL = (2654435761, 2246822519, 3266489917, 668265263, 374761393)
 
 
-def widekeys_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+def _mix32(ent, j: int):
+    """A 32-bit hash of entity ids (int64 tensor, values < 2^32; murmur3's finaliser over ent * m_j + j): the
+    dimension values of distinct entities are independent, so ~every entity is its own 5-column group. (Through
+    round 5 the dimensions were (ent * m_j + j) mod card_j: every cardinality divides 20000, so the 5-tuple was a
+    function of ent mod 20000 -- at most ~20K distinct groups, not the ~1M entities the workload describes.)"""
+    m = 0xFFFFFFFF
+    x = (ent * _WIDE_MUL[j] + j * 0x27D4EB2F) & m
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & m
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & m
+    return x ^ (x >> 16)
+
+
+def widekeys_segment(name: str, num_docs: int, seed: int, device: str = "cuda", uniform: bool = False) -> S.SegmentBuffers:
     """Segment of the wide-key table: entity e ~ Zipf(1.1) over WIDE_ENTITIES ranks (inverse-CDF of the
-    continuous Pareto approximation), dimension j = (e * m_j + j) mod card_j as a fixed-bit dictionary column
-    (the first card_j docs take every dictionary value once), raw INT / DOUBLE metrics."""
+    continuous Pareto approximation) -- or, uniform=True, uniform over them (no hot keys: the unskewed case of
+    the map-based holders) -- dimension j = (e * m_j + j) mod card_j as a fixed-bit dictionary column (the first
+    card_j docs take every dictionary value once), raw INT / DOUBLE metrics."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     n = num_docs
     u = torch.rand((n,), generator=g, device=device, dtype=torch.float64)
-    s_ = 1.1
-    a = WIDE_ENTITIES ** (1.0 - s_)
-    ent = torch.clamp(((a - 1.0) * u + 1.0) ** (1.0 / (1.0 - s_)), 1.0, float(WIDE_ENTITIES)).to(torch.int64) - 1
+    if uniform:
+        ent = torch.clamp((u * WIDE_ENTITIES).to(torch.int64), 0, WIDE_ENTITIES - 1)
+    else:
+        s_ = 1.1
+        a = WIDE_ENTITIES ** (1.0 - s_)
+        ent = torch.clamp(((a - 1.0) * u + 1.0) ** (1.0 / (1.0 - s_)), 1.0, float(WIDE_ENTITIES)).to(torch.int64) - 1
     cols = {}
     for j, (cname, card) in enumerate(zip(WIDE_COLUMNS, WIDE_CARDS)):
-        ids = ((ent * _WIDE_MUL[j] + j) % card).to(torch.int32)
+        ids = (_mix32(ent, j) % card).to(torch.int32)
         ids[:card] = torch.arange(card, device=device, dtype=torch.int32)
         bits = S.num_bits_per_value(card - 1)
         dvals = np.arange(card, dtype=np.int32)
@@ -162,6 +180,11 @@ def widekeys_segment(name: str, num_docs: int, seed: int, device: str = "cuda") 
 
 WIDEKEYS_QUERY = ("SET numGroupsLimit = 2000000000; SELECT w1, w2, w3, w4, w5, COUNT(*), SUM(metInt), MAX(metDouble) "
                   "FROM wide WHERE metInt < 900 GROUP BY w1, w2, w3, w4, w5")
+def widekeys_uniform_segment(name: str, num_docs: int, seed: int, device: str = "cuda") -> S.SegmentBuffers:
+    """The wide-key table with entities uniform over WIDE_ENTITIES (~1M groups, none hot)."""
+    return widekeys_segment(name, num_docs, seed, device, uniform=True)
+
+
 WIDEKEYS_BYTES_PER_ROW = sum(S.num_bits_per_value(c - 1) for c in WIDE_CARDS) / 8.0 + 4 + 8
 
 

@@ -19,6 +19,7 @@ args_for() {
     highcard) echo "--workload highcard --segments 40" ;;
     hcdef) echo "--workload highcard-default --segments 40" ;;
     widekeys) echo "--workload wide-keys --segments 40" ;;
+    wku) echo "--workload wide-keys-uniform --segments 40" ;;
     inv1[0-9]) echo "--workload inverted --segments 40 --query-index ${1#inv}" ;;
     inv[0-9]) echo "--workload inverted --segments 40 --query-index ${1#inv}" ;;
     ssb[0-9]|ssb1[0-2]) echo "--workload ssb --segments 20 --query-index ${1#ssb}" ;;

@@ -118,3 +118,33 @@ def test_spill_regions_grow_after_an_overflow(wide, monkeypatch):
     assert r1.groups() == exp
     r2 = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
     assert r2.groups() == exp
+
+
+@pytest.fixture(scope="module")
+def wide_uniform():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    from pinot_amd import engine as E
+    bufs = [datagen.widekeys_uniform_segment(f"wu{i}", 300_000 + 11 * i, seed=70 + i) for i in range(2)]
+    _, exp = oracle.execute(datagen.WIDEKEYS_QUERY, bufs)
+    return E, bufs, [E.ImmutableSegment(b) for b in bufs], exp
+
+
+@pytest.mark.parametrize("env", [{}, {"PINOT_AMD_HASH_LDS": "0"}, {"PINOT_AMD_HASH_SPILL": "0"},
+                                 {"PINOT_AMD_SPILL_BYTES": "4096"}],
+                         ids=["default", "nolds", "nospill", "spill-overflow"])
+def test_widekeys_uniform_vs_oracle(wide_uniform, env, monkeypatch):
+    """Wide keys without skew (entities uniform over 1M ranks: ~450K groups in 600K docs, no key hot enough for an
+    on-die first level): the hash plan the key-distribution sample picks, and the fixed alternatives."""
+    E, bufs, segs, exp = wide_uniform
+    monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    res = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
+    assert "hash" in res.kernel_info(), res.kernel_info()
+    got = res.groups()
+    assert len(got) == len(exp) > 200_000
+    assert got == exp
+    assert sum(v[0] for v in got.values()) == res.num_docs_matched()
+    res.execute_again()
+    assert res.groups() == exp
