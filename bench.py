@@ -120,6 +120,10 @@ PLAN_KERNELS = {
     "jit-partitioned": "pinot_part_scatter+pinot_part_agg (+pinot_part_count, or the direct-atomic pinot_scan_jit on handover)",
     "jit-hash": "pinot_scan_jit (LDS-privatised first level + HBM hash table)",
     "jit-hash-trim": "pinot_scan_jit (HBM hash table keyed by segment) + trim_* + hash_merge_kernel",
+    "jit-hash+nolds": "pinot_scan_jit (no LDS level: every matching doc spilled to its block's region) + "
+                      "spill_scatter_sorted_kernel + spill_agg_kernel",
+    "jit-hash+direct": "pinot_scan_jit (no LDS level: records placed straight into their key-hash partitions) + "
+                       "spill_agg_kernel",
 }
 
 

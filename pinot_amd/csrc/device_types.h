@@ -180,6 +180,17 @@ struct DevHash {
   uint32_t* spill_hist;              // [partition * grid + block] records kept in the region
   int32_t spill_shift;               // partitions = 2^(64 - spill_shift)
   int32_t spill_words;
+  // Direct placement (JitPlan::hash_direct with direct = 1; keys without skew, no LDS first level): a record goes
+  // straight to its place in the partition-major array -- dst + dbase[p * grid + b] + the block's running count of
+  // partition p -- from the exact per-(partition, block) counts dcnt of an earlier region-mode execution of the same
+  // plan (the doc -> (partition, block) map is fixed: no LDS level decides which docs spill). Records past a count
+  // take the HBM table; a block whose count of some partition falls short of dcnt leaves holes and adds to check
+  // (the result is then void: pinot_amd_result_check_word / verify).
+  unsigned long long* dst;
+  const int64_t* dbase;
+  const uint32_t* dcnt;
+  unsigned long long* check;
+  int32_t direct;
 };
 constexpr int kSpillMaxParts = 2048;  // spill partitions (the scan block's LDS histogram)
 

@@ -56,6 +56,10 @@ hipError_t launch_admit(uint32_t* first, int64_t nk, const uint32_t* seen, const
 hipError_t launch_presence_bitset(const uint64_t* count, int64_t n, unsigned long long* bits, hipStream_t st);
 hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
                           unsigned long long* cut, hipStream_t st);
+hipError_t launch_spill_direct_prep(const int64_t* offs, const int64_t* part_begin, const uint32_t* hist, int P,
+                                    int64_t grid, int64_t* dbase, uint32_t* dcnt, int64_t* pbeg, hipStream_t st);
+hipError_t launch_spill_agg(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
+                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, hipStream_t st);
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
                                int agg_grid, int S, int sorted_scatter, hipStream_t st);
@@ -142,6 +146,7 @@ static const std::set<std::string>& kept_knobs() {
       "PINOT_AMD_GENERIC_BITS",
       "PINOT_AMD_GROUP_PLAN",
       "PINOT_AMD_HASH_CAP_CACHE",
+      "PINOT_AMD_HASH_DIRECT",
       "PINOT_AMD_HASH_INIT_SLOTS",
       "PINOT_AMD_HASH_LDS",
       "PINOT_AMD_HASH_LDS_ADMIT",
@@ -1425,6 +1430,13 @@ struct Launch {
   JitKernel* jit = nullptr;         // scan, or the partitioned count / scatter / aggregate trio
   JitKernel* jit_atomic = nullptr;  // partitioned: direct-atomic scan used when few docs match
   JitKernel* jit_sample = nullptr;  // partitioned: match count over every sample_stride-th tile
+  // hash plans with a second level: the scan without the LDS level (JitPlan::hash_direct), its LDS bytes, and
+  // the direct placement's per-launch tables (DevHash::dbase / dcnt, the partition begins) with the partition
+  // count (log2) they were made for
+  JitKernel* jit_direct = nullptr;
+  size_t shmem_direct = 0;
+  DevBuf d_dbase, d_dcnt, d_dpbeg;
+  int direct_lg = -1;
   int grid = 1, atomic_grid = 1, sample_grid = 1, agg_grid = 1, scan_nsub = 1, part_sub = kPartSub;
   size_t shmem = 0, shmem_scatter = 0, shmem_agg = 0;
   DevPartition part{};
@@ -1502,6 +1514,12 @@ struct pinot_amd_result {
   // partitioned GROUP BY: shared work buffers (launches run one after another)
   DevBuf hist, offs, part_begin, rec;
   bool check_failed = false;  // the last execution's partitioned self-check failed (verify_partitioned)
+  // hash plans with a second level: 0 = the LDS level (skewed keys), 1 = no LDS level, records to the blocks'
+  // regions (counting the direct placement's allotments), 2 = direct placement; 0 -> 1 when an execution spilled
+  // most matching docs (check_overflow), 1 -> 2 after a counting execution. direct_ran: the last execution placed
+  // records directly (its check word then holds the blocks that fell short of their allotments)
+  int hash_mode = 0;
+  bool direct_ran = false;
   // prepared-plan cache (plan_cache_*): the identity this plan was built for, the segments it reads, its device bytes
   std::string plan_key;
   std::vector<uint64_t> plan_uids;
@@ -2370,8 +2388,9 @@ static int launch_one(pinot_amd_result* r, Launch& L, size_t li, uint64_t* table
     return 0;
   }
   if (r->kind != PLAN_PARTITIONED) {
-    HIP_OK(hipModuleLaunchKernel(L.jit->fn, (unsigned)L.grid, 1, 1, kBlock * L.scan_nsub, 1, 1, (unsigned)L.shmem, st, args,
-                                 nullptr));
+    const bool direct = r->hash_mode > 0 && L.jit_direct;  // (the same grid: the spill regions are sized for it)
+    HIP_OK(hipModuleLaunchKernel(direct ? L.jit_direct->fn : L.jit->fn, (unsigned)L.grid, 1, 1, kBlock * L.scan_nsub, 1, 1,
+                                 (unsigned)(direct ? L.shmem_direct : L.shmem), st, args, nullptr));
     return 0;
   }
   const unsigned pt = (unsigned)(kBlock * L.part_sub);
@@ -2571,6 +2590,7 @@ static int grow_hash(pinot_amd_result* r, bool* grown) {
 static int run_plan(pinot_amd_result* r) {
   r->merged = false;
   r->check_failed = false;
+  r->direct_ran = false;
   r->ovf_pending = false;
   hipStream_t st = r->stream;
   r->compacted = false;
@@ -2635,11 +2655,44 @@ static int run_plan(pinot_amd_result* r) {
       H.overflow = overflow;
       for (size_t li = 0; li < nl; ++li)
         if (r->launches[li].batch == b) {
-          if (int rc = launch_one(r, r->launches[li], li, table, H)) return rc;
-          if (!r->trim && r->spill_words > 0)
-            HIP_OK(launch_spill_passes(H, r->nw, r->launches[li].grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
+          Launch& L = r->launches[li];
+          DevHash HL = H;
+          const bool dmode = !r->trim && r->spill_words > 0 && r->hash_mode > 0 && L.jit_direct;
+          const int lg = 64 - H.spill_shift;
+          if (dmode && r->hash_mode == 2 && L.direct_lg == lg) {  // records straight to their places
+            HL.direct = 1;
+            HL.dst = (unsigned long long*)r->sp_sorted.p;
+            HL.dbase = (const int64_t*)L.d_dbase.p;
+            HL.dcnt = (const uint32_t*)L.d_dcnt.p;
+            HL.check = ctr + 3 * nl + 2;
+            r->direct_ran = true;
+          }
+          if (int rc = launch_one(r, L, li, table, HL)) return rc;
+          if (HL.direct) {
+            HIP_OK(launch_spill_agg(HL, r->nw, (const unsigned long long*)r->sp_sorted.p, (const int64_t*)L.d_dpbeg.p, r->q,
+                                    (uint64_t*)r->acc.p, r->spill_agg_grid, r->spill_slots, st));
+          } else if (!r->trim && r->spill_words > 0) {
+            HIP_OK(launch_spill_passes(HL, r->nw, L.grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
                                        (unsigned long long*)r->sp_sorted.p, r->q, (uint64_t*)r->acc.p, r->spill_agg_grid,
                                        r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "0") ? 0 : 1, st));
+            if (dmode) {  // this region-mode execution without the LDS level counted the direct placement's allotments
+              const size_t cells = ((size_t)1 << lg) * (size_t)L.grid;
+              if (L.d_dbase.n < cells * 8) {
+                L.d_dbase.reset();
+                L.d_dcnt.reset();
+                if (int rc = L.d_dbase.alloc(cells * 8)) return rc;
+                if (int rc = L.d_dcnt.alloc(cells * 4)) return rc;
+              }
+              if (L.d_dpbeg.n < (((size_t)1 << lg) + 1) * 8) {
+                L.d_dpbeg.reset();
+                if (int rc = L.d_dpbeg.alloc((((size_t)1 << lg) + 1) * 8)) return rc;
+              }
+              HIP_OK(launch_spill_direct_prep((const int64_t*)r->sp_offs.p, (const int64_t*)r->sp_pbeg.p,
+                                              (const uint32_t*)r->sp_hist.p, 1 << lg, L.grid, (int64_t*)L.d_dbase.p,
+                                              (uint32_t*)L.d_dcnt.p, (int64_t*)L.d_dpbeg.p, st));
+              L.direct_lg = lg;
+            }
+          }
         }
       if (r->trim) {
         const int32_t nb = r->batch_nsegs[b];
@@ -2686,6 +2739,7 @@ static int run_plan(pinot_amd_result* r) {
     if (!grown) break;  // at the ceiling: the overflow counter stays set, the result reports EOVERFLOW
     HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
    }
+    if (r->hash_mode == 1) r->hash_mode = 2;  // the allotments are counted: the next execution places directly
   } else {
     if (r->admit)
       if (int rc = run_admission(r, limit_flag)) return rc;
@@ -4165,6 +4219,17 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     }
     L.jit = jit_get(jp, &r->jit_status);
     if (!L.jit) return fail(PINOT_AMD_EUNSUPPORTED, "scan kernel unavailable: %s", r->jit_status.c_str());
+    if (jp.hash && jp.hash_spill && jp.hash_lds > 0 && !env_is("PINOT_AMD_HASH_DIRECT", "0")) {
+      // the same scan without the LDS level, for keys without skew (a 64-slot table stays for the shared code)
+      JitPlan jd = jp;
+      jd.hash_direct = true;
+      jd.hash_lds = 64;
+      jd.hash_admit = 0;
+      std::string err;
+      L.jit_direct = jit_get(jd, &err);  // absent: the LDS-level plan serves every execution
+      L.shmem_direct = (size_t)(hash_lds_bytes / jp.hash_lds) * 64;
+      if (L.jit_direct && env_is("PINOT_AMD_HASH_DIRECT", "force")) r->hash_mode = 1;  // (tests: from the first execution)
+    }
     if (r->admit) {
       // the admission's first-doc pass: the launch's filter + group key over each segment's prefix
       JitPlan jf = jp;
@@ -4240,6 +4305,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       }
     }
     if (!jp.select) L.shmem += L.shmem_sets;  // a select pass has no table: its sets start at 0
+    if (L.jit_direct) L.shmem_direct += L.shmem_sets;
     int per_cu = 1;
     if (jp.partitioned) {
       JitPlan ja = jp;  // companion direct-atomic scan for batches where the filter keeps few docs
@@ -4740,7 +4806,18 @@ static std::string selfcheck_report(pinot_amd_result* r) {
 // counts are never read. There is no re-execution: the cause of the round-5 misreads is gone (module loads, jit.cpp
 // jit_get), and any future failure must surface, with the blocks' placement, instead of being retried away.
 static int verify_partitioned(pinot_amd_result* r, const std::vector<unsigned long long>& c) {
-  if (r->kind != PLAN_PARTITIONED || r->check_failed) return r->check_failed ? fail(PINOT_AMD_EINVAL, "%s", r->check_msg.c_str()) : 0;
+  if (r->check_failed) return fail(PINOT_AMD_EINVAL, "%s", r->check_msg.c_str());
+  if (r->kind == PLAN_HASH && r->direct_ran) {  // direct placement: every block filled its allotments
+    const unsigned long long bad = c[3 * r->launches.size() + 2];
+    if (bad == 0) return 0;
+    r->check_failed = true;
+    ++g_selfcheck_failures;
+    r->check_msg = "hash plan direct placement: " + std::to_string(bad) +
+                   " (partition, block) allotments got fewer records than the counting execution made; the result is void";
+    fprintf(stderr, "pinot_amd: %s\n", r->check_msg.c_str());
+    return fail(PINOT_AMD_EINVAL, "%s", r->check_msg.c_str());
+  }
+  if (r->kind != PLAN_PARTITIONED) return 0;
   const unsigned long long bad = c[3 * r->launches.size() + 2];
   if (bad == 0) return 0;
   r->check_failed = true;
@@ -4802,6 +4879,9 @@ const char* pinot_amd_result_kernel_info(pinot_amd_result* r) {
     case PLAN_HASH: info = r->trim ? "jit-hash-trim" : "jit-hash"; break;
     default: info = "jit";
   }
+  // the hash plan's second level: the LDS level dropped, counting (region) or placing directly -- as of the next
+  // execution for the counting step (the mode advances at the end of an execution)
+  if (r->kind == PLAN_HASH && r->hash_mode > 0) info += r->direct_ran ? "+direct" : "+nolds";
   for (const auto& L : r->launches)
     if (L.select) {
       // wselect: the filter ran on 64-doc words; fwselect: fused with the inverted-index expansion
@@ -4858,6 +4938,14 @@ static int check_overflow(pinot_amd_result* r) {
     HIP_OK(hipStreamSynchronize(st));
     const int64_t mx = (int64_t)*std::max_element(cnt.begin(), cnt.end());
     if (mx > r->spill_cap) remember_spill_capacity(r->cap_key, mx + mx / 8);
+    // most matching docs missed the LDS level (keys without skew): the next executions drop it -- one counting the
+    // blocks' records per partition, then direct placement (no region pass)
+    bool all_direct = !r->launches.empty();
+    for (const Launch& L : r->launches) all_direct &= L.jit_direct != nullptr;
+    const size_t last = r->launches.size() - 1;
+    int64_t spilled = 0;
+    for (uint32_t x : cnt) spilled += x;
+    if (r->hash_mode == 0 && all_direct && c[3 * last] > 0 && 2 * spilled >= (int64_t)c[3 * last]) r->hash_mode = 1;
   }
   if (r->sel_ctr.n) {
     std::vector<unsigned long long> sc(r->sel_ctr.n / 8);

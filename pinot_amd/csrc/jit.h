@@ -135,6 +135,10 @@ struct JitPlan {
   // with hash_lds: a key that finds no LDS slot is spilled (DevHash::spill: appended as a record and counted
   // per key-hash partition) instead of probing the HBM table per doc
   bool hash_spill = false;
+  // with hash_spill: no LDS level (keys without skew miss it anyway); every matching doc is spilled, to its
+  // block's region (DevHash::direct = 0, which leaves exact per-(partition, block) counts) or straight to its
+  // place in the partition-major array (direct = 1, from those counts), the region pass then skipped
+  bool hash_direct = false;
   // selection-vector plan: pinot_select (the filter over the filter columns, appending matching docIds)
   // + pinot_gather (decodes only the group-by / aggregated columns of those docs and aggregates)
   bool select = false;

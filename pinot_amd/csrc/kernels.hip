@@ -1910,6 +1910,38 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
   return hipGetLastError();
 }
 
+// Direct placement's tables (DevHash::direct) from a region-mode execution's spill passes: record place
+// dbase[p * grid + b] = part_begin[p] + offs[p * grid + b], its count dcnt = the block's records of partition p, and
+// the partition begins the aggregation reads (part_begin is shared by the launches of a plan; these are per launch)
+__global__ void spill_direct_prep_kernel(const int64_t* offs, const int64_t* part_begin, const uint32_t* hist, int P,
+                                         int64_t grid, int64_t* dbase, uint32_t* dcnt, int64_t* pbeg) {
+  const int64_t n = (int64_t)P * grid;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    dbase[i] = part_begin[i / grid] + offs[i];
+    dcnt[i] = hist[i];
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= P; i += (int64_t)gridDim.x * blockDim.x)
+    pbeg[i] = part_begin[i];
+}
+
+hipError_t launch_spill_direct_prep(const int64_t* offs, const int64_t* part_begin, const uint32_t* hist, int P,
+                                    int64_t grid, int64_t* dbase, uint32_t* dcnt, int64_t* pbeg, hipStream_t st) {
+  hipLaunchKernelGGL(spill_direct_prep_kernel, dim3(grid_cap((int64_t)P * grid, kBlock, 4096)), dim3(kBlock), 0, st, offs,
+                     part_begin, hist, P, grid, dbase, dcnt, pbeg);
+  return hipGetLastError();
+}
+
+// the second level's aggregation alone: records already partition-major (direct placement)
+hipError_t launch_spill_agg(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
+                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, hipStream_t st) {
+  const int P = 1 << (64 - H.spill_shift);
+  const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
+  (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, sorted, part_begin, P, nw,
+                     H.spill_words, S, q, H, acc);
+  return hipGetLastError();
+}
+
 hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
                           unsigned long long* cut, hipStream_t st) {
   if (nsegs <= 0) return hipSuccess;
