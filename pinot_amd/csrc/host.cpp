@@ -1520,6 +1520,7 @@ struct pinot_amd_result {
   // records directly (its check word then holds the blocks that fell short of their allotments)
   int hash_mode = 0;
   bool direct_ran = false;
+  bool direct_place = false;  // mode 2 allowed (PINOT_AMD_HASH_DIRECT=place / force)
   // prepared-plan cache (plan_cache_*): the identity this plan was built for, the segments it reads, its device bytes
   std::string plan_key;
   std::vector<uint64_t> plan_uids;
@@ -2657,7 +2658,7 @@ static int run_plan(pinot_amd_result* r) {
         if (r->launches[li].batch == b) {
           Launch& L = r->launches[li];
           DevHash HL = H;
-          const bool dmode = !r->trim && r->spill_words > 0 && r->hash_mode > 0 && L.jit_direct;
+          const bool dmode = !r->trim && r->spill_words > 0 && r->hash_mode > 0 && L.jit_direct && r->direct_place;
           const int lg = 64 - H.spill_shift;
           if (dmode && r->hash_mode == 2 && L.direct_lg == lg) {  // records straight to their places
             HL.direct = 1;
@@ -2739,7 +2740,7 @@ static int run_plan(pinot_amd_result* r) {
     if (!grown) break;  // at the ceiling: the overflow counter stays set, the result reports EOVERFLOW
     HIP_OK(hipMemsetAsync(r->matched.p, 0, r->matched.n, st));
    }
-    if (r->hash_mode == 1) r->hash_mode = 2;  // the allotments are counted: the next execution places directly
+    if (r->hash_mode == 1 && r->direct_place) r->hash_mode = 2;  // allotments counted: the next execution places directly
   } else {
     if (r->admit)
       if (int rc = run_admission(r, limit_flag)) return rc;
@@ -3883,7 +3884,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     const int64_t slot_bytes = (int64_t)(base.hash_words + lds_arrays()) * 8;
     // second level: the LDS misses spilled as records and aggregated per key-hash partition (kernels.hip
     // spill passes) instead of one HBM probe + atomics per doc; PINOT_AMD_HASH_SPILL=0 keeps the direct path
-    const bool spill = !env_is("PINOT_AMD_HASH_SPILL", "0");
+    int nval = 0;  // a spill record's value words (spill_agg_kernel holds at most 8 words of a record)
+    for (const JitAcc& a : base.accs) nval += a.op != ACC_HI && a.op != ACC_FIRST_DOC;
+    const bool spill = !env_is("PINOT_AMD_HASH_SPILL", "0") && base.hash_words + nval <= 8;
     const int64_t reserve = 1024 + (spill ? (int64_t)kSpillMaxParts * 4 + 16 : 0);
     // as many slots as the LDS holds beside the kernel's static LDS (counters), a multiple of 64
     int64_t S = env_i64("PINOT_AMD_HASH_LDS_SLOTS", 0);
@@ -4229,6 +4232,7 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       L.jit_direct = jit_get(jd, &err);  // absent: the LDS-level plan serves every execution
       L.shmem_direct = (size_t)(hash_lds_bytes / jp.hash_lds) * 64;
       if (L.jit_direct && env_is("PINOT_AMD_HASH_DIRECT", "force")) r->hash_mode = 1;  // (tests: from the first execution)
+      r->direct_place = env_is("PINOT_AMD_HASH_DIRECT", "force") || env_is("PINOT_AMD_HASH_DIRECT", "place");
     }
     if (r->admit) {
       // the admission's first-doc pass: the launch's filter + group key over each segment's prefix

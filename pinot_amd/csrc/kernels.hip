@@ -122,12 +122,16 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 }
 // slot of the nw-word key kw in a table (inserted if absent; lock-free word-by-word CAS, see
 // DevHash), -1 when every slot holds another key
-__device__ int64_t hash_find_rt(unsigned long long* keys, int64_t cap, int nw, const uint64_t* kw) {
+// max_probe > 0: give up after that many slots (a crowded table: the caller counts the doc as overflow and the
+// host grows the table) -- unbounded, every new key of a full table walked all of it (a cold wide-key execution
+// whose first table was too small spent 68 s in one spill aggregation)
+__device__ int64_t hash_find_rt(unsigned long long* keys, int64_t cap, int nw, const uint64_t* kw, int64_t max_probe = 0) {
   uint64_t x = 0x9E3779B97F4A7C15ull;
   for (int w = 0; w < nw; ++w) x = fmix64(x ^ kw[w]);
   const uint64_t mask = (uint64_t)cap - 1ull;
   uint64_t i = x & mask;
-  for (int64_t n = 0; n < cap; ++n) {
+  const int64_t lim = max_probe > 0 && max_probe < cap ? max_probe : cap;
+  for (int64_t n = 0; n < lim; ++n) {
     bool ok = true;
     for (int w = 0; w < nw && ok; ++w) {
       unsigned long long* pw = keys + (uint64_t)w * (uint64_t)cap + i;
@@ -534,7 +538,9 @@ __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, 
 // LDS-sorted variant (PINOT_AMD_SPILL_SORT=1): the block counting-sorts chunks of C records of its region by
 // partition in LDS, then writes the chunk word by word in partition order -- consecutive lanes store
 // consecutive words of a partition's run, instead of one 8-byte store per lane and word into 64 scattered
-// runs. C = 1024 x per records (per = 1 or 2 per thread).
+// runs. C = 1024 x per records (per = 1..kSortPerMax per thread, as many as the LDS holds: with ~1K partitions a
+// chunk of 2048 records gave each partition 2-record runs, partial 128-B lines written back 1.6x over).
+constexpr int kSortPerMax = 8;
 __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
                                                                     const int64_t* part_begin, unsigned long long* out,
                                                                     int per) {
@@ -555,8 +561,15 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
     const int m = (int)min((int64_t)C, n - c0);
     for (int i = tid; i < P; i += 1024) cnt[i] = 0u;
     __syncthreads();
-    int pr[2] = {-1, -1}, rk[2] = {0, 0};
-    for (int h = 0; h < per; ++h) {
+    int pr[kSortPerMax], rk[kSortPerMax];
+#pragma unroll
+    for (int h = 0; h < kSortPerMax; ++h) {
+      pr[h] = -1;
+      rk[h] = 0;
+    }
+#pragma unroll
+    for (int h = 0; h < kSortPerMax; ++h) {
+      if (h >= per) break;
       const int i = tid + h * 1024;
       if (i >= m) continue;
       const unsigned long long* r = reg + (c0 + i) * W;
@@ -583,8 +596,9 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
       if (i0 + 1 < P) start[i0 + 1] = ex + a;
     }
     __syncthreads();
-    for (int h = 0; h < per; ++h) {
-      if (pr[h] < 0) continue;
+#pragma unroll
+    for (int h = 0; h < kSortPerMax; ++h) {
+      if (h >= per || pr[h] < 0) continue;
       const int i = tid + h * 1024, pos = (int)start[pr[h]] + rk[h];
       const unsigned long long* r = reg + (c0 + i) * W;
       for (int w = 0; w < W; ++w) stage[(size_t)pos * W + w] = r[w];
@@ -612,6 +626,8 @@ __device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* p
 // records (a key that finds no slot within 64 probes goes to the HBM table directly), then every occupied
 // slot is merged into the HBM table (AggregationFunction.merge: counts and sums add, MIN / MAX by the ordered
 // encoding) and the table is cleared for the next partition.
+constexpr int kSpillPreU = 4;  // spill_agg_kernel: records per thread and step
+constexpr int kSpillPreW = 8;  // record words held in registers (launch_spill_* require spill_words <= 8)
 __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long long* recs, const int64_t* part_begin,
                                                          int P, int nw, int W, int S, DevQuery q, DevHash H,
                                                          uint64_t* acc) {
@@ -634,16 +650,24 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
     pi = lo;
   }
   const int nacc = q.nacc;
+  __shared__ int WJ[kMaxAcc];  // record word of accumulator a's value (acc order, ACC_HI skipped)
+  if (tid == 0) {
+    int j = nw;
+    for (int a = 0; a < nacc && a < kMaxAcc; ++a) WJ[a] = (a == 0 || q.acc_op[a] == ACC_HI) ? -1 : j++;
+  }
+  __syncthreads();
   while (r0 < r1) {
     while (part_begin[pi + 1] <= r0) ++pi;
     const int64_t pe = min(r1, part_begin[pi + 1]);
     for (int i = tid; i < nw * S; i += blockDim.x) LK[i] = ~0ull;
     for (int i = tid; i < nacc * S; i += blockDim.x) LA[i] = acc_identity(q.acc_op[i / S]);
     __syncthreads();
-    for (int64_t i = r0 + tid; i < pe; i += blockDim.x) {
-      const unsigned long long* r = recs + i * W;
+    // one record (its words in rw, statically indexed) into the partition's LDS table, or the HBM table
+    auto agg_one = [&](const uint64_t (&rw)[kSpillPreW]) {
       uint64_t kw[kMaxKeyWords];
-      for (int w = 0; w < nw; ++w) kw[w] = r[w];
+#pragma unroll
+      for (int w = 0; w < kSpillPreW; ++w)
+        if (w < nw) kw[w] = rw[w];
       const uint64_t x = key_hash_rt(kw, nw);
       uint32_t s = (uint32_t)(((x & 0xFFFFFFFFull) * (uint64_t)(uint32_t)S) >> 32);
       int ls = -1;
@@ -667,31 +691,50 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
         }
         s = s + 1u == (uint32_t)S ? 0u : s + 1u;
       }
+      auto word = [&](int j) {  // record word j through selects (no dynamic register indexing)
+        uint64_t v = 0ull;
+#pragma unroll
+        for (int w = 0; w < kSpillPreW; ++w) v = w == j ? rw[w] : v;
+        return v;
+      };
       if (ls >= 0) {  // the LDS slot (the accumulator words addressed from the shared array: LDS atomics)
         atomicAdd(reinterpret_cast<unsigned long long*>(LA + ls), 1ull);
-        int j = nw;
         for (int a = 1; a < nacc; ++a) {
           const int32_t op = q.acc_op[a];
           if (op == ACC_HI) continue;
-          spill_apply(op, LA + (int64_t)a * S + ls, LA + (int64_t)(a + 1 < nacc ? a + 1 : a) * S + ls, r[j++]);
+          spill_apply(op, LA + (int64_t)a * S + ls, LA + (int64_t)(a + 1 < nacc ? a + 1 : a) * S + ls, word(WJ[a]));
         }
-        continue;
+        return;
       }
       // no LDS slot: straight into the HBM table
-      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
+      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw, H.max_probe);
       if (slot < 0) {
         atomicAdd(H.overflow, 1ull);
-        continue;
+        return;
       }
       uint64_t* base = acc + slot;
       const int64_t stride = H.cap;
       atomicAdd(reinterpret_cast<unsigned long long*>(base), 1ull);
-      int j = nw;
       for (int a = 1; a < nacc; ++a) {
         const int32_t op = q.acc_op[a];
         if (op == ACC_HI) continue;
-        spill_apply(op, base + (int64_t)a * stride, base + (int64_t)(a + 1 < nacc ? a + 1 : a) * stride, r[j++]);
+        spill_apply(op, base + (int64_t)a * stride, base + (int64_t)(a + 1 < nacc ? a + 1 : a) * stride, word(WJ[a]));
       }
+    };
+    // kSpillPreU records per thread and step, every word loaded before any is aggregated (the loads of a step
+    // overlap instead of each record's waiting behind the previous one's LDS atomics)
+    for (int64_t i0 = r0; i0 < pe; i0 += (int64_t)kSpillPreU * blockDim.x) {
+      uint64_t rw[kSpillPreU][kSpillPreW];
+#pragma unroll
+      for (int u = 0; u < kSpillPreU; ++u) {
+        const int64_t i = i0 + (int64_t)u * blockDim.x + tid;
+        const unsigned long long* r = recs + (i < pe ? i : r0) * W;
+#pragma unroll
+        for (int w = 0; w < kSpillPreW; ++w) rw[u][w] = w < W ? r[w] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kSpillPreU; ++u)
+        if (i0 + (int64_t)u * blockDim.x + tid < pe) agg_one(rw[u]);
     }
     __syncthreads();
     for (int ls = tid; ls < S; ls += blockDim.x) {
@@ -699,7 +742,7 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
       if (c == 0ull) continue;
       uint64_t kw[kMaxKeyWords];
       for (int w = 0; w < nw; ++w) kw[w] = LK[(int64_t)w * S + ls];
-      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw);
+      const int64_t slot = hash_find_rt(H.keys, H.cap, nw, kw, H.max_probe);
       if (slot < 0) {
         atomicAdd(H.overflow, c);
         continue;
@@ -1893,7 +1936,8 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
   const auto sorted_lds = [&](int per) {
     return (size_t)1024 * per * H.spill_words * 8 + (size_t)P * (8 + 4 + 4) + (size_t)1024 * per * 2;
   };
-  const int per = sorted_lds(2) <= (size_t)150 * 1024 ? 2 : 1;
+  int per = kSortPerMax;
+  while (per > 1 && sorted_lds(per) > (size_t)150 * 1024) --per;
   if (sorted_scatter && sorted_lds(per) <= (size_t)150 * 1024) {
     (void)hipFuncSetAttribute((const void*)spill_scatter_sorted_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sorted_lds(per));

@@ -151,11 +151,11 @@ def test_widekeys_uniform_vs_oracle(wide_uniform, env, monkeypatch):
 
 
 def test_widekeys_uniform_drops_the_lds_level(wide_uniform, monkeypatch):
-    """Most docs of a uniform key distribution miss the LDS level: after the first execution the plan drops it --
-    the next execution spills every doc to its block's region and so counts each (partition, block) allotment, the
-    ones after place each record straight into the partition-major array (no region pass). Every step exact."""
+    """Most docs of a uniform key distribution miss the LDS level: after the first execution the plan drops it and
+    spills every matching doc to its block's region (no LDS probe per doc). Every step exact."""
     E, bufs, segs, exp = wide_uniform
     monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")
+    monkeypatch.setenv("PINOT_AMD_HASH_DIRECT", "auto")  # (also a plan identity of its own: no prepared plan)
     res = E.ServerQueryExecutor().execute(datagen.WIDEKEYS_QUERY, segs)
     assert "+nolds" not in res.kernel_info() and "+direct" not in res.kernel_info()
     assert res.groups() == exp  # (the fetch sees most docs spilled: the LDS level goes)
@@ -164,7 +164,7 @@ def test_widekeys_uniform_drops_the_lds_level(wide_uniform, monkeypatch):
     assert res.groups() == exp
     for _ in range(2):
         res.execute_again()
-        assert "+direct" in res.kernel_info(), res.kernel_info()
+        assert "+nolds" in res.kernel_info(), res.kernel_info()
         assert res.groups() == exp
         assert sum(v[0] for v in res.groups().values()) == res.num_docs_matched()
 
@@ -174,7 +174,9 @@ def test_widekeys_uniform_drops_the_lds_level(wide_uniform, monkeypatch):
                                  {"PINOT_AMD_HASH_DIRECT": "force", "PINOT_AMD_SPILL_BYTES": "65536"}],
                          ids=["force", "force-grow", "force-small-regions"])
 def test_widekeys_direct_placement_forced(wide, wide_uniform, env, monkeypatch):
-    """Direct placement from the first execution on, over skewed and uniform keys; with a table that grows while the
+    """Direct placement (PINOT_AMD_HASH_DIRECT=force: no LDS level from the first execution, which counts the
+    (partition, block) allotments; the later ones place each record straight into its partition, no region pass),
+    over skewed and uniform keys; with a table that grows while the
     plan runs (the partition count changes: the allotments are counted again) and with spill regions too small for
     the counting execution (records past them take the HBM table; the direct one places exactly what was counted)."""
     monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")
