@@ -5061,6 +5061,7 @@ int pinot_amd_result_num_groups_limit_reached(pinot_amd_result* r, int32_t* h_ou
   if (r->num_group_by == 0 || !r->limit_possible) return 0;
   std::vector<unsigned long long> c;
   if (int rc = read_counters(r, &c)) return rc;
+  if (int rc = verify_partitioned(r, c)) return rc;  // a void execution reports no flag either
   *h_out = c[3 * r->launches.size()] != 0 ? 1 : 0;
   return 0;
 }
