@@ -59,10 +59,10 @@ hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t
 hipError_t launch_spill_direct_prep(const int64_t* offs, const int64_t* part_begin, const uint32_t* hist, int P,
                                     int64_t grid, int64_t* dbase, uint32_t* dcnt, int64_t* pbeg, hipStream_t st);
 hipError_t launch_spill_agg(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
-                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, hipStream_t st);
+                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, uint32_t narrow, hipStream_t st);
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
-                               int agg_grid, int S, int sorted_scatter, hipStream_t st);
+                               int agg_grid, int S, int sorted_scatter, uint32_t narrow, hipStream_t st);
 hipError_t launch_gather_groups(const int32_t* slots, int64_t ngroups, const unsigned long long* keys, int nw,
                                 int64_t cap, const uint64_t* acc, int32_t nacc, uint64_t* out_keys, uint64_t* out_acc,
                                 hipStream_t st);
@@ -1553,6 +1553,7 @@ struct pinot_amd_result {
   int64_t spill_cap = 0, spill_grid = 0;
   int64_t spill_cap_max = 0;  // regions' ceiling: the scan blocks' docs, within PINOT_AMD_SPILL_MAX_BYTES
   int spill_words = 0, spill_slots = 0, spill_agg_grid = 1;
+  uint32_t spill_narrow = 0;  // accumulators (bit a) whose integer sums fit int64 over all docs: plain LDS adds
   bool cap_known = false, ovf_pending = false;
   bool trim = false;                   // numGroupsLimit trimming (scan tables keyed by (key, segment))
   int64_t limit = 100000;
@@ -2671,11 +2672,11 @@ static int run_plan(pinot_amd_result* r) {
           if (int rc = launch_one(r, L, li, table, HL)) return rc;
           if (HL.direct) {
             HIP_OK(launch_spill_agg(HL, r->nw, (const unsigned long long*)r->sp_sorted.p, (const int64_t*)L.d_dpbeg.p, r->q,
-                                    (uint64_t*)r->acc.p, r->spill_agg_grid, r->spill_slots, st));
+                                    (uint64_t*)r->acc.p, r->spill_agg_grid, r->spill_slots, r->spill_narrow, st));
           } else if (!r->trim && r->spill_words > 0) {
             HIP_OK(launch_spill_passes(HL, r->nw, L.grid, nullptr, (int64_t*)r->sp_offs.p, (int64_t*)r->sp_pbeg.p,
                                        (unsigned long long*)r->sp_sorted.p, r->q, (uint64_t*)r->acc.p, r->spill_agg_grid,
-                                       r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "0") ? 0 : 1, st));
+                                       r->spill_slots, env_is("PINOT_AMD_SPILL_SORT", "0") ? 0 : 1, r->spill_narrow, st));
             if (dmode) {  // this region-mode execution without the LDS level counted the direct placement's allotments
               const size_t cells = ((size_t)1 << lg) * (size_t)L.grid;
               if (L.d_dbase.n < cells * 8) {
@@ -3880,6 +3881,12 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     // |value| fit (the HBM path of the same kernel always adds 128 bits); the grid has >= min(CUs, tiles / 4)
     // blocks
     const int64_t min_grid = std::max<int64_t>(1, std::min<int64_t>(cus, all_tiles / kPartSub));
+    // the second level's LDS tables may meet every doc of the batch: their integer sums stay int64 when all docs x
+    // |value| fit (spill_agg_kernel's narrow mask)
+    set_narrow((__int128)std::max<int64_t>(all_docs, 1));
+    r->spill_narrow = 0;
+    for (size_t i = 0; i < base.accs.size() && i + 1 < 32; ++i)
+      if (base.accs[i].narrow) r->spill_narrow |= 1u << (i + 1);
     set_narrow((__int128)((all_tiles + min_grid - 1) / min_grid) * kTileDocs);
     const int64_t slot_bytes = (int64_t)(base.hash_words + lds_arrays()) * 8;
     // second level: the LDS misses spilled as records and aggregated per key-hash partition (kernels.hip

@@ -626,11 +626,12 @@ __device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* p
 // records (a key that finds no slot within 64 probes goes to the HBM table directly), then every occupied
 // slot is merged into the HBM table (AggregationFunction.merge: counts and sums add, MIN / MAX by the ordered
 // encoding) and the table is cleared for the next partition.
+__device__ __forceinline__ uint64_t spill_sext(int64_t v) { return v < 0 ? ~0ull : 0ull; }
 constexpr int kSpillPreU = 4;  // spill_agg_kernel: records per thread and step
 constexpr int kSpillPreW = 8;  // record words held in registers (launch_spill_* require spill_words <= 8)
 __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long long* recs, const int64_t* part_begin,
                                                          int P, int nw, int W, int S, DevQuery q, DevHash H,
-                                                         uint64_t* acc) {
+                                                         uint64_t* acc, uint32_t narrow) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lt[];
   unsigned long long* LK = lt;                         // nw x S key words
   uint64_t* LA = (uint64_t*)(lt + (int64_t)nw * S);    // q.nacc x S accumulators
@@ -702,7 +703,10 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
         for (int a = 1; a < nacc; ++a) {
           const int32_t op = q.acc_op[a];
           if (op == ACC_HI) continue;
-          spill_apply(op, LA + (int64_t)a * S + ls, LA + (int64_t)(a + 1 < nacc ? a + 1 : a) * S + ls, word(WJ[a]));
+          if ((narrow >> a) & 1u)  // a narrow integer SUM: an int64 partial in LDS, no carry (no returning atomic)
+            atomicAdd(reinterpret_cast<unsigned long long*>(LA + (int64_t)a * S + ls), (unsigned long long)word(WJ[a]));
+          else
+            spill_apply(op, LA + (int64_t)a * S + ls, LA + (int64_t)(a + 1 < nacc ? a + 1 : a) * S + ls, word(WJ[a]));
         }
         return;
       }
@@ -749,7 +753,7 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
       }
       for (int a = 0; a < nacc; ++a) {
         const uint64_t v = LA[(int64_t)a * S + ls];
-        const uint64_t vh = a + 1 < nacc ? LA[(int64_t)(a + 1) * S + ls] : 0ull;
+        const uint64_t vh = ((narrow >> a) & 1u) ? spill_sext((int64_t)v) : a + 1 < nacc ? LA[(int64_t)(a + 1) * S + ls] : 0ull;
         acc_apply(q.acc_op[a], acc + (uint64_t)a * (uint64_t)H.cap + slot,
                   acc + (uint64_t)(a + 1 < nacc ? a + 1 : a) * (uint64_t)H.cap + slot, v, vh);
       }
@@ -1927,7 +1931,7 @@ hipError_t launch_segsel(const unsigned long long* keys, int64_t cap, int nw, co
 
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
-                               int agg_grid, int S, int sorted_scatter, hipStream_t st) {
+                               int agg_grid, int S, int sorted_scatter, uint32_t narrow, hipStream_t st) {
   (void)hist_unused;
   const int P = 1 << (64 - H.spill_shift);
   // offsets of (partition, block) runs, partition-major (the histogram the scan left in H.spill_hist)
@@ -1950,7 +1954,7 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
   const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
   (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, (const unsigned long long*)sorted,
-                     (const int64_t*)part_begin, P, nw, H.spill_words, S, q, H, acc);
+                     (const int64_t*)part_begin, P, nw, H.spill_words, S, q, H, acc, narrow);
   return hipGetLastError();
 }
 
@@ -1977,12 +1981,12 @@ hipError_t launch_spill_direct_prep(const int64_t* offs, const int64_t* part_beg
 
 // the second level's aggregation alone: records already partition-major (direct placement)
 hipError_t launch_spill_agg(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
-                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, hipStream_t st) {
+                            const DevQuery& q, uint64_t* acc, int agg_grid, int S, uint32_t narrow, hipStream_t st) {
   const int P = 1 << (64 - H.spill_shift);
   const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
   (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, sorted, part_begin, P, nw,
-                     H.spill_words, S, q, H, acc);
+                     H.spill_words, S, q, H, acc, narrow);
   return hipGetLastError();
 }
 
