@@ -156,7 +156,7 @@ def committed_traffic(query: str, kernel_info: str, rows: int):
     gfx950 correction of MI355X_MICROARCH.md) + WRITE_SIZE, per row of the profiled run, scaled to `rows`.
     A record of another plan (a planner change since the pass) is not used: traffic is then None."""
     sha = query_sha1(query)
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         pmc = os.path.join(ROOT, "profiles", rnd, "pmc_index.json")
         if not os.path.exists(pmc):
             continue
