@@ -220,15 +220,16 @@ int pinot_amd_query_set_result_limit(pinot_amd_query* q, int64_t limit, int64_t 
  * Pinot's sorted combine (CombinePlanNode.java:150-154) keeps the top LIMIT groups, exact; at or above it each
  * segment keeps its top LIMIT groups by the ORDER BY (GroupByOperator.java:157-175) and the combine table the
  * top trimSize of their union -- restated for dense key spaces (a presence pass over ORDER BY ranks, each
- * segment's LIMIT-th rank as the cutoff its docs are aggregated within); over a hash-table key space execute
- * returns EUNSUPPORTED when some segment could hold more than LIMIT groups. */
+ * segment's LIMIT-th rank as the cutoff its docs are aggregated within) and over hash-table key spaces (the
+ * (key, segment) scan table, each segment's top LIMIT entries by a radix selection over the ORDER BY). */
 int pinot_amd_query_set_server_options(pinot_amd_query* q, int32_t server_return_final_result,
                                        int64_t sort_aggregate_limit_threshold);
 /* QueryOptions minSegmentGroupTrimSize (default -1: CommonConstants.java:1436). With ORDER BY not equal to the
- * GROUP BY keys (an unsafe trim) and a positive value, each segment would keep its top max(value, 5 x LIMIT)
- * groups by the ORDER BY, aggregation values included (QueryContext.java:575-578): that trim is not restated,
- * so execute returns EUNSUPPORTED when some segment could hold more groups than that. Under a safe trim the
- * segment trim size is LIMIT whatever this value (pinot_amd_query_set_server_options). */
+ * GROUP BY keys (an unsafe trim) and a positive value, each segment keeps its top max(value, 5 x LIMIT) groups
+ * by the ORDER BY, aggregation values included (QueryContext.java:575-578, GroupByUtils.java:63-66): the (key,
+ * segment) hash plan, each segment's top entries by a radix selection over the ORDER BY's final values (ties in
+ * ascending group key; TableResizer leaves them unspecified). Under a safe trim the segment trim size is LIMIT
+ * whatever this value (pinot_amd_query_set_server_options). */
 int pinot_amd_query_set_segment_trim(pinot_amd_query* q, int64_t min_segment_group_trim_size);
 /* ORDER BY key of the server table, in order of precedence: kind 0 = group-by column `index` (value
  * order), kind 1 = aggregation `index` (final value, Double.compare); ascending != 0 for ASC. */
@@ -254,6 +255,9 @@ int pinot_amd_result_bitset(pinot_amd_result* r, int32_t segment_index, const ui
 /* Re-run a query whose plan was compiled by pinot_amd_execute on the same segments (no host work
  * beyond the launches): the benchmarked step. */
 int pinot_amd_execute_again(pinot_amd_result* r, void* stream);
+/* Release a result after synchronising its stream. Its plan is kept (idle, up to PINOT_AMD_PLAN_CACHE_BYTES of
+ * plan device memory) for the next pinot_amd_execute of the same query -- every field, the same segments, the
+ * same device and planner overrides -- which then only runs it; destroying a segment drops the plans over it. */
 int pinot_amd_result_destroy(pinot_amd_result* r);
 /* Number of docs that matched the filter across all segments (numDocsScanned). */
 int pinot_amd_result_num_docs_matched(pinot_amd_result* r, int64_t* h_out);
