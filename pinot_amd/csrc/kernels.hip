@@ -539,7 +539,9 @@ __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, 
 // partition in LDS, then writes the chunk word by word in partition order -- consecutive lanes store
 // consecutive words of a partition's run, instead of one 8-byte store per lane and word into 64 scattered
 // runs. C = 1024 x per records (per = 1..kSortPerMax per thread, as many as the LDS holds: with ~1K partitions a
-// chunk of 2048 records gave each partition 2-record runs, partial 128-B lines written back 1.6x over).
+// chunk of 2048 records gave each partition 2-record runs, partial 128-B lines written back 1.6x over). The chunk is
+// read from HBM once, coalesced, into LDS in record order; the sort only permutes indices (srt) -- reading each
+// record again for the copy fetched the chunk twice once chunks outgrew the L2 (FETCH 15.6 GB for 7.9 GB of records).
 constexpr int kSortPerMax = 8;
 __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
                                                                     const int64_t* part_begin, unsigned long long* out,
@@ -552,6 +554,7 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
   uint32_t* cnt = (uint32_t*)(base + P);                          // P: the chunk's records per partition
   uint32_t* start = cnt + P;                                      // P: their exclusive prefix
   uint16_t* pid = (uint16_t*)(start + P);                         // C: partition of each sorted slot
+  uint16_t* srt = pid + C;                                        // C: chunk record index of each sorted slot
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t b = blockIdx.x;
   for (int i = tid; i < P; i += 1024) base[i] = part_begin[i] + offs[(int64_t)i * grid + b];
@@ -560,6 +563,7 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
   for (int64_t c0 = 0; c0 < n; c0 += C) {
     const int m = (int)min((int64_t)C, n - c0);
     for (int i = tid; i < P; i += 1024) cnt[i] = 0u;
+    for (int j = tid; j < m * W; j += 1024) stage[j] = reg[c0 * W + j];  // the chunk's words, record order
     __syncthreads();
     int pr[kSortPerMax], rk[kSortPerMax];
 #pragma unroll
@@ -572,9 +576,8 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
       if (h >= per) break;
       const int i = tid + h * 1024;
       if (i >= m) continue;
-      const unsigned long long* r = reg + (c0 + i) * W;
       uint64_t kw[kMaxKeyWords];
-      for (int w = 0; w < nw; ++w) kw[w] = r[w];
+      for (int w = 0; w < nw; ++w) kw[w] = stage[(size_t)i * W + w];
       pr[h] = (int)(key_hash_rt(kw, nw) >> H.spill_shift);
       rk[h] = (int)atomicAdd(&cnt[pr[h]], 1u);
     }
@@ -600,14 +603,13 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
     for (int h = 0; h < kSortPerMax; ++h) {
       if (h >= per || pr[h] < 0) continue;
       const int i = tid + h * 1024, pos = (int)start[pr[h]] + rk[h];
-      const unsigned long long* r = reg + (c0 + i) * W;
-      for (int w = 0; w < W; ++w) stage[(size_t)pos * W + w] = r[w];
+      srt[pos] = (uint16_t)i;
       pid[pos] = (uint16_t)pr[h];
     }
     __syncthreads();
     for (int j = tid; j < m * W; j += 1024) {
       const int pos = j / W, w = j - pos * W, p = pid[pos];
-      out[(size_t)(base[p] + (pos - (int)start[p])) * W + w] = stage[j];
+      out[(size_t)(base[p] + (pos - (int)start[p])) * W + w] = stage[(size_t)srt[pos] * W + w];
     }
     __syncthreads();
     for (int i = tid; i < P; i += 1024) base[i] += cnt[i];
@@ -1938,7 +1940,7 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
   hipLaunchKernelGGL(partition_row_scan_kernel, dim3((unsigned)P), dim3(kBlock), 0, st, H.spill_hist, grid, offs, part_begin);
   hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(kBlock), 0, st, part_begin, (int64_t)P, part_begin + P);
   const auto sorted_lds = [&](int per) {
-    return (size_t)1024 * per * H.spill_words * 8 + (size_t)P * (8 + 4 + 4) + (size_t)1024 * per * 2;
+    return (size_t)1024 * per * H.spill_words * 8 + (size_t)P * (8 + 4 + 4) + (size_t)1024 * per * 2 * 2;
   };
   int per = kSortPerMax;
   while (per > 1 && sorted_lds(per) > (size_t)150 * 1024) --per;
