@@ -140,20 +140,24 @@ def _predicate_spec(pred, column: ColumnBuffers, use_inverted: bool, keep: list)
             else:
                 setattr(s, side + "_d", v)
         return s
-    vals = [_coerce(v, st) for v in pred.values]
-    s.num_values = len(vals)
+    s.num_values = len(pred.values)
     if st == STRING:
+        vals = [_coerce(v, st) for v in pred.values]
         arr = (C.c_char_p * len(vals))(*[v.encode() for v in vals])
         keep.append(arr)
         s.h_values_s = arr
     elif st in (INT, LONG):
-        arr = (C.c_int64 * len(vals))(*vals)
+        # numpy buffers handed over by pointer: a ctypes array built element by element cost ~0.5 us per literal
+        if all(type(v) is int for v in pred.values):
+            arr = np.asarray(pred.values, dtype=np.int64)
+        else:
+            arr = np.asarray([_coerce(v, st) for v in pred.values], dtype=np.int64)
         keep.append(arr)
-        s.h_values_i = arr
+        s.h_values_i = arr.ctypes.data_as(C.POINTER(C.c_int64))
     else:
-        arr = (C.c_double * len(vals))(*vals)
+        arr = np.asarray([_coerce(v, st) for v in pred.values], dtype=np.float64)
         keep.append(arr)
-        s.h_values_d = arr
+        s.h_values_d = arr.ctypes.data_as(C.POINTER(C.c_double))
     return s
 
 
