@@ -1433,6 +1433,7 @@ struct Launch {
   // hash plans with a second level: the scan without the LDS level (JitPlan::hash_direct), its LDS bytes, and
   // the direct placement's per-launch tables (DevHash::dbase / dcnt, the partition begins) with the partition
   // count (log2) they were made for
+  std::vector<DevSegment> h_segs;  // the uploaded descriptors (self-check forensics compare the count blocks' reads)
   JitKernel* jit_direct = nullptr;
   size_t shmem_direct = 0;
   DevBuf d_dbase, d_dcnt, d_dpbeg;
@@ -4028,6 +4029,8 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
     L.q.nsegs = (int32_t)L.segs.size();
     L.q.total_tiles = tiles;
     if (int rc = L.d_segs.alloc_copy(ls.data(), ls.size() * sizeof(DevSegment), 0)) return rc;
+    static_assert(sizeof(DevSegment) % 8 == 0, "the count pass checksums descriptors in 8-byte words");
+    L.h_segs = ls;
     // fused when few docs match (measured: 0.01 % / 0.1 % of 1B rows 0.36 / 0.52 -> 0.24 / 0.42 ms; at
     // 1 % the separate expansion's occupancy wins, 1.08 vs 1.17 ms); PINOT_AMD_FUSED_INV_SELECT=1 forces it
     double lm = 0, ld = 0;
@@ -4738,6 +4741,19 @@ static std::string selfcheck_report(pinot_amd_result* r) {
         for (int64_t c = b * kPartCountRatio; c < (b + 1) * kPartCountRatio && c < cg; ++c) {
           for (int64_t q = 0; q < P; ++q) counted += hist[(size_t)q * cg + c];
           out += "; count block " + std::to_string(c) + " (" + where(c) + ")";
+          // the descriptors it read (checksummed as it read them) against the plan's upload
+          const uint32_t rng = hw[(size_t)c * kHwWords + 3];
+          const int s0 = (int)(rng >> 16), s1 = (int)(rng & 0xFFFFu);
+          if (rng != 0 || hw[(size_t)c * kHwWords + 2] != 0) {
+            uint64_t dk = 0xcbf29ce484222325ull;
+            for (int k = s0; k <= s1 && k < (int)L.h_segs.size(); ++k) {
+              const uint64_t* w = (const uint64_t*)&L.h_segs[(size_t)k];
+              for (size_t i = 0; i < sizeof(DevSegment) / 8; ++i) dk = (dk ^ w[i]) * 0x100000001b3ull;
+            }
+            const bool same = (uint32_t)(dk ^ (dk >> 32)) == hw[(size_t)c * kHwWords + 2];
+            out += std::string(same ? ", read its descriptors as planned" : ", READ DESCRIPTORS OTHER THAN THE PLAN'S") +
+                   " (segments " + std::to_string(s0) + "-" + std::to_string(s1) + ")";
+          }
         }
         out += "; counted " + std::to_string(counted);
       }
