@@ -6,6 +6,8 @@
 # PINOT_AMD_JIT_PROBE_UNLOAD=0 (one load, nothing unloaded); AB=2: PINOT_AMD_JIT_PROBE_UNLOAD=2 (the probe module
 # stays loaded: two live modules of one image, nothing unloaded) against the load as built; AB=3: kernel arguments
 # in host memory (HIP_FORCE_DEV_KERNARG=0) against the load as built.
+# (Recreate the worktree first: git worktree add build/r5pre 98a21d2, plus the A/B knobs of the round-6 records;
+# removed at the end of round 6.)
 set -o pipefail
 O=$PWD/gpurun_out/r6_cache_ab
 mkdir -p $O
