@@ -3907,6 +3907,9 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       // 22.1 -> 15.4 ms, the LDS slots then holding the Zipf head instead of the first keys seen
       // (profiles/r05/sweep_wk_cap.txt); PINOT_AMD_HASH_LDS_ADMIT=n sets 2^-n, 0 inserts every key
       base.hash_admit = (int)std::min<int64_t>(8, std::max<int64_t>(0, env_i64("PINOT_AMD_HASH_LDS_ADMIT", 5)));
+      // 4 of the 8 slots a one-word key could probe at once: on the ~1M-group Zipf table 16.65 -> 15.45 ms per 1B
+      // rows (2 probes: 17.0; profiles/r06/sweep_lds_probes.txt) -- a key past 4 slots spills instead of reading 4 more
+      base.hash_probes = 4;
       base.scan_nsub = kPartSub;
       hash_lds_bytes = S * slot_bytes;
     } else {

@@ -172,6 +172,7 @@ struct JitPlan {
   // hash plans' LDS first level: a doc may insert its key into an EMPTY slot with probability 2^-hash_admit
   // (0: always) -- admission by recurrence, so the slots hold a skewed distribution's head
   int hash_admit = 0;
+  int hash_probes = kHashLdsProbes;  // LDS-level slots a doc's key probes before it spills (<= kHashLdsProbes)
   // diagnostics only (PINOT_AMD_DIAG_ADMIT_OFF): the dense admission's per-doc bitmap lookup left out (wrong
   // results; isolates the lookup's traffic in A/B profiles)
   bool diag_admit_off = false;
