@@ -174,9 +174,9 @@ struct DevHash {
   // encoding) -- and counted in its key-hash partition (hash >> spill_shift). The spill passes (kernels.hip)
   // then group the records by partition and aggregate each partition in LDS, so the tail keys reach the HBM
   // table once per (partition chunk, key) instead of once per doc. Records past spill_cap take the HBM table.
-  unsigned long long* spill;         // grid x spill_cap records of spill_words words
-  int64_t spill_cap;
-  uint32_t* spill_cnt;               // per block: records appended (those past spill_cap counted too)
+  unsigned long long* spill;         // grid x kSpillGroups sub-regions of spill_cap records of spill_words words
+  int64_t spill_cap;                 // records per sub-region
+  uint32_t* spill_cnt;               // per sub-region: records appended (those past spill_cap counted too)
   uint32_t* spill_hist;              // [partition * grid + block] records kept in the region
   int32_t spill_shift;               // partitions = 2^(64 - spill_shift)
   int32_t spill_words;
@@ -193,6 +193,10 @@ struct DevHash {
   int32_t direct;
 };
 constexpr int kSpillMaxParts = 2048;  // spill partitions (the scan block's LDS histogram)
+// A scan block's spill region is split in kSpillGroups sub-regions by the partition's top 2 bits (sub-region
+// bx * kSpillGroups + g, spill_cap records each, spill_cnt per sub-region): a chunk of the region pass then meets a
+// quarter of the partitions, so its partition runs are 4x longer (whole 128-byte lines instead of ~5-record runs)
+constexpr int kSpillGroups = 4;
 
 // Segment-level group trim over a hash plan's (key, segment) scan table (GroupByOperator.java:157-175,
 // TableResizer.trimInSegmentResults): each segment keeps its top `keep` groups in the ORDER BY's order. The order is

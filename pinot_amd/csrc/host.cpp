@@ -2602,7 +2602,7 @@ static int run_plan(pinot_amd_result* r) {
     // ones are freed first: hipFree waits for the work still reading them)
     const int64_t want = std::min(known_spill_capacity(r->cap_key), r->spill_cap_max);
     if (want > r->spill_cap) {
-      const size_t bytes = (size_t)r->spill_grid * (size_t)want * (size_t)r->spill_words * 8;
+      const size_t bytes = (size_t)r->spill_grid * kSpillGroups * (size_t)want * (size_t)r->spill_words * 8;
       r->sp_rec.reset();
       r->sp_sorted.reset();
       if (int rc = r->sp_rec.alloc(bytes)) return rc;
@@ -4518,20 +4518,25 @@ static int execute_impl(pinot_amd_query* qq, pinot_amd_segment* const* segs_in, 
       int nval = 0;
       for (const JitAcc& a : base.accs) nval += a.op != ACC_HI && a.op != ACC_FIRST_DOC;
       r->spill_words = r->nw + nval;
+      // (sizes per sub-region: a block's region is kSpillGroups of them, one per partition group -- a quarter of the
+      // block's docs each when the spilled keys hash evenly, with a quarter more for the spread)
       const double budget = (double)env_i64("PINOT_AMD_SPILL_BYTES", (int64_t)8 << 30);
-      r->spill_cap = std::max<int64_t>(64, std::min<int64_t>(per_max * kTileDocs,
-                                                              (int64_t)(budget / ((double)gmax * r->spill_words * 8.0))));
+      const int64_t block_docs = per_max * kTileDocs;
+      const int64_t sub_docs = block_docs / kSpillGroups + block_docs / (4 * kSpillGroups) + 256;
+      r->spill_cap = std::max<int64_t>(64, std::min<int64_t>(std::min(sub_docs, block_docs),
+          (int64_t)(budget / ((double)gmax * kSpillGroups * r->spill_words * 8.0))));
       // an earlier execution of this query shape over these segments needed more (its regions overflowed): up to
       // PINOT_AMD_SPILL_MAX_BYTES (default 32 GiB per copy); run_plan grows them the same way later
       const double maxb = (double)env_i64("PINOT_AMD_SPILL_MAX_BYTES", (int64_t)32 << 30);
-      r->spill_cap_max = std::max<int64_t>(64, std::min<int64_t>(per_max * kTileDocs,
-                                                                  (int64_t)(maxb / ((double)gmax * r->spill_words * 8.0))));
+      r->spill_cap_max = std::max<int64_t>(64, std::min<int64_t>(block_docs,
+          (int64_t)(maxb / ((double)gmax * kSpillGroups * r->spill_words * 8.0))));
       if (const int64_t known = known_spill_capacity(r->cap_key))
         r->spill_cap = std::max(r->spill_cap, std::min(known, r->spill_cap_max));
       r->spill_grid = gmax;
-      if (int rc = r->sp_rec.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
-      if (int rc = r->sp_sorted.alloc((size_t)gmax * (size_t)r->spill_cap * (size_t)r->spill_words * 8)) return rc;
-      if (int rc = r->sp_cnt.alloc((size_t)gmax * 4)) return rc;
+      const size_t region_bytes = (size_t)gmax * kSpillGroups * (size_t)r->spill_cap * (size_t)r->spill_words * 8;
+      if (int rc = r->sp_rec.alloc(region_bytes)) return rc;
+      if (int rc = r->sp_sorted.alloc(region_bytes)) return rc;
+      if (int rc = r->sp_cnt.alloc((size_t)gmax * kSpillGroups * 4)) return rc;
       if (int rc = r->sp_hist.alloc((size_t)kSpillMaxParts * (size_t)gmax * 4)) return rc;
       if (int rc = r->sp_offs.alloc((size_t)kSpillMaxParts * (size_t)gmax * 8)) return rc;
       if (int rc = r->sp_pbeg.alloc(((size_t)kSpillMaxParts + 1) * 8)) return rc;
@@ -4963,7 +4968,7 @@ static int check_overflow(pinot_amd_result* r) {
                 (long long)c[3 * r->launches.size() + 1]);
   if (r->spill_words > 0 && r->spill_grid > 0 && !r->cap_key.empty()) {
     // the last launch's per-block record counts: a region that ran out sizes the next execution's regions
-    std::vector<uint32_t> cnt((size_t)r->spill_grid);
+    std::vector<uint32_t> cnt((size_t)r->spill_grid * kSpillGroups);
     HIP_OK(hipMemcpyAsync(cnt.data(), r->sp_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     const int64_t mx = (int64_t)*std::max_element(cnt.begin(), cnt.end());

@@ -518,12 +518,12 @@ __device__ __forceinline__ uint64_t key_hash_rt(const uint64_t* kw, int nw) {
 __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
                                                              const int64_t* part_begin, unsigned long long* out) {
   extern __shared__ uint32_t cur[];
-  const int64_t b = blockIdx.x;
+  const int64_t sr = blockIdx.x, b = sr / kSpillGroups;  // sub-region sr of scan block b (one partition group)
   const int P = 1 << (64 - H.spill_shift), W = H.spill_words;
   for (int i = threadIdx.x; i < P; i += blockDim.x) cur[i] = 0u;
   __syncthreads();
-  const int64_t n = min((int64_t)H.spill_cnt[b], H.spill_cap);
-  const unsigned long long* reg = H.spill + b * H.spill_cap * W;
+  const int64_t n = min((int64_t)H.spill_cnt[sr], H.spill_cap);
+  const unsigned long long* reg = H.spill + sr * H.spill_cap * W;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
     const unsigned long long* r = reg + i * W;
     uint64_t kw[kMaxKeyWords];
@@ -556,10 +556,10 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
   uint16_t* pid = (uint16_t*)(start + P);                         // C: partition of each sorted slot
   uint16_t* srt = pid + C;                                        // C: chunk record index of each sorted slot
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t b = blockIdx.x;
+  const int64_t sr = blockIdx.x, b = sr / kSpillGroups;  // sub-region sr of scan block b: a quarter of the partitions
   for (int i = tid; i < P; i += 1024) base[i] = part_begin[i] + offs[(int64_t)i * grid + b];
-  const int64_t n = min((int64_t)H.spill_cnt[b], H.spill_cap);
-  const unsigned long long* reg = H.spill + b * H.spill_cap * W;
+  const int64_t n = min((int64_t)H.spill_cnt[sr], H.spill_cap);
+  const unsigned long long* reg = H.spill + sr * H.spill_cap * W;
   for (int64_t c0 = 0; c0 < n; c0 += C) {
     const int m = (int)min((int64_t)C, n - c0);
     for (int i = tid; i < P; i += 1024) cnt[i] = 0u;
@@ -1947,10 +1947,10 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
   if (sorted_scatter && sorted_lds(per) <= (size_t)150 * 1024) {
     (void)hipFuncSetAttribute((const void*)spill_scatter_sorted_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sorted_lds(per));
-    hipLaunchKernelGGL(spill_scatter_sorted_kernel, dim3((unsigned)grid), dim3(1024), sorted_lds(per), st, H, nw, grid,
+    hipLaunchKernelGGL(spill_scatter_sorted_kernel, dim3((unsigned)(grid * kSpillGroups)), dim3(1024), sorted_lds(per), st, H, nw, grid,
                        (const int64_t*)offs, (const int64_t*)part_begin, sorted, per);
   } else {
-    hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)grid), dim3(1024), (size_t)P * 4, st, H, nw, grid,
+    hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)(grid * kSpillGroups)), dim3(1024), (size_t)P * 4, st, H, nw, grid,
                        (const int64_t*)offs, (const int64_t*)part_begin, sorted);
   }
   const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
