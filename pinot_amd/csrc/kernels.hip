@@ -543,6 +543,7 @@ __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, 
 // read from HBM once, coalesced, into LDS in record order; the sort only permutes indices (srt) -- reading each
 // record again for the copy fetched the chunk twice once chunks outgrew the L2 (FETCH 15.6 GB for 7.9 GB of records).
 constexpr int kSortPerMax = 8;
+constexpr int kSortPrefWords = 6;  // a chunk's first words per thread prefetched into registers (8: VGPR spills)
 __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
                                                                     const int64_t* part_begin, unsigned long long* out,
                                                                     int per) {
@@ -562,10 +563,28 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
   for (int i = tid; i < P; i += 1024) base[i] = part_begin[i] + offs[(int64_t)i * grid + b];
   const int64_t n = min((int64_t)H.spill_cnt[sr], H.spill_cap);
   const unsigned long long* reg = H.spill + sr * H.spill_cap * W;
+  // the next chunk's first kSortPrefWords words per thread are loaded into registers once the current chunk is
+  // sorted, so those HBM reads overlap this chunk's write phase (the CU holds one block: its phases would otherwise
+  // run serially); a chunk of more words loads the rest when it is staged
+  unsigned long long nx[kSortPrefWords];
+  const auto load_chunk = [&](int64_t c) {
+    const int mw = (int)min((int64_t)C, n - c) * W;
+#pragma unroll
+    for (int i = 0; i < kSortPrefWords; ++i) {
+      const int j = tid + i * 1024;
+      if (j < mw) nx[i] = reg[c * W + j];
+    }
+  };
+  if (n > 0) load_chunk(0);
   for (int64_t c0 = 0; c0 < n; c0 += C) {
     const int m = (int)min((int64_t)C, n - c0);
     for (int i = tid; i < P; i += 1024) cnt[i] = 0u;
-    for (int j = tid; j < m * W; j += 1024) stage[j] = reg[c0 * W + j];  // the chunk's words, record order
+#pragma unroll
+    for (int i = 0; i < kSortPrefWords; ++i) {  // the chunk's words, record order: the prefetched ones, the rest
+      const int j = tid + i * 1024;
+      if (j < m * W) stage[j] = nx[i];
+    }
+    for (int j = tid + kSortPrefWords * 1024; j < m * W; j += 1024) stage[j] = reg[c0 * W + j];
     __syncthreads();
     int pr[kSortPerMax], rk[kSortPerMax];
 #pragma unroll
@@ -608,6 +627,7 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
       srt[pos] = (uint16_t)i;
       pid[pos] = (uint16_t)pr[h];
     }
+    if (c0 + C < n) load_chunk(c0 + C);
     __syncthreads();
     for (int j = tid; j < m * W; j += 1024) {
       const int pos = (W == 1 ? j : (int)__umulhi((uint32_t)j, wmagic)), w = j - pos * W, p = pid[pos];
