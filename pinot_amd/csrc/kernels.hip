@@ -543,7 +543,15 @@ __global__ void __launch_bounds__(1024) spill_scatter_kernel(DevHash H, int nw, 
 // read from HBM once, coalesced, into LDS in record order; the sort only permutes indices (srt) -- reading each
 // record again for the copy fetched the chunk twice once chunks outgrew the L2 (FETCH 15.6 GB for 7.9 GB of records).
 constexpr int kSortPerMax = 8;
-constexpr int kSortPrefWords = 6;  // a chunk's first words per thread prefetched into registers (8: VGPR spills)
+constexpr int kSortPrefWords = 12;  // a chunk's first words per thread prefetched into registers (W = 3: all)
+// Workgroup barrier ordering LDS only (waits for the wave's LDS operations, not for its global loads in flight:
+// __syncthreads()'s fence waits vmcnt(0), which would drain a prefetch at every barrier)
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, int nw, int64_t grid, const int64_t* offs,
                                                                     const int64_t* part_begin, unsigned long long* out,
                                                                     int per) {
@@ -563,16 +571,18 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
   for (int i = tid; i < P; i += 1024) base[i] = part_begin[i] + offs[(int64_t)i * grid + b];
   const int64_t n = min((int64_t)H.spill_cnt[sr], H.spill_cap);
   const unsigned long long* reg = H.spill + sr * H.spill_cap * W;
-  // the next chunk's first kSortPrefWords words per thread are loaded into registers once the current chunk is
-  // sorted, so those HBM reads overlap this chunk's write phase (the CU holds one block: its phases would otherwise
-  // run serially); a chunk of more words loads the rest when it is staged
+  // the next chunk's first kSortPrefWords words per thread are loaded into registers as soon as the current chunk
+  // is staged, so those HBM reads overlap this chunk's sort and write phases (the CU holds one block: its phases
+  // would otherwise run serially; the loop's barriers order LDS only, so they do not wait for the loads); a chunk of
+  // more words loads the rest when it is staged
   unsigned long long nx[kSortPrefWords];
   const auto load_chunk = [&](int64_t c) {
     const int mw = (int)min((int64_t)C, n - c) * W;
+    const unsigned long long* rb = reg + c * W;
 #pragma unroll
     for (int i = 0; i < kSortPrefWords; ++i) {
-      const int j = tid + i * 1024;
-      if (j < mw) nx[i] = reg[c * W + j];
+      const uint32_t j = (uint32_t)tid + (uint32_t)i * 1024u;
+      if ((int)j < mw) nx[i] = rb[j];
     }
   };
   if (n > 0) load_chunk(0);
@@ -585,13 +595,11 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
       if (j < m * W) stage[j] = nx[i];
     }
     for (int j = tid + kSortPrefWords * 1024; j < m * W; j += 1024) stage[j] = reg[c0 * W + j];
-    __syncthreads();
-    int pr[kSortPerMax], rk[kSortPerMax];
+    lds_sync();
+    if (c0 + C < n) load_chunk(c0 + C);
+    uint32_t prk[kSortPerMax];  // a record's partition (high half) and rank in it (low half); ~0 = none
 #pragma unroll
-    for (int h = 0; h < kSortPerMax; ++h) {
-      pr[h] = -1;
-      rk[h] = 0;
-    }
+    for (int h = 0; h < kSortPerMax; ++h) prk[h] = ~0u;
 #pragma unroll
     for (int h = 0; h < kSortPerMax; ++h) {
       if (h >= per) break;
@@ -599,10 +607,10 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
       if (i >= m) continue;
       uint64_t kw[kMaxKeyWords];
       for (int w = 0; w < nw; ++w) kw[w] = stage[(size_t)i * W + w];
-      pr[h] = (int)(key_hash_rt(kw, nw) >> H.spill_shift);
-      rk[h] = (int)atomicAdd(&cnt[pr[h]], 1u);
+      const uint32_t pr = (uint32_t)(key_hash_rt(kw, nw) >> H.spill_shift);
+      prk[h] = (pr << 16) | atomicAdd(&cnt[pr], 1u);
     }
-    __syncthreads();
+    lds_sync();
     {  // exclusive prefix of the counts (P <= 2048: two entries per thread)
       const int i0 = tid * 2;
       const uint32_t a = i0 < P ? cnt[i0] : 0u, a2 = i0 + 1 < P ? cnt[i0 + 1] : 0u;
@@ -612,30 +620,30 @@ __global__ void __launch_bounds__(1024) spill_scatter_sorted_kernel(DevHash H, i
         if (lane >= o) x += y;
       }
       if (lane == 63) wsum[wv] = x;
-      __syncthreads();
+      lds_sync();
       uint32_t off = 0;
       for (int k = 0; k < wv; ++k) off += wsum[k];
       const uint32_t ex = off + x - (a + a2);
       if (i0 < P) start[i0] = ex;
       if (i0 + 1 < P) start[i0 + 1] = ex + a;
     }
-    __syncthreads();
+    lds_sync();
 #pragma unroll
     for (int h = 0; h < kSortPerMax; ++h) {
-      if (h >= per || pr[h] < 0) continue;
-      const int i = tid + h * 1024, pos = (int)start[pr[h]] + rk[h];
+      if (h >= per || prk[h] == ~0u) continue;
+      const uint32_t pr = prk[h] >> 16;
+      const int i = tid + h * 1024, pos = (int)start[pr] + (int)(prk[h] & 0xFFFFu);
       srt[pos] = (uint16_t)i;
-      pid[pos] = (uint16_t)pr[h];
+      pid[pos] = (uint16_t)pr;
     }
-    if (c0 + C < n) load_chunk(c0 + C);
-    __syncthreads();
+    lds_sync();
     for (int j = tid; j < m * W; j += 1024) {
       const int pos = (W == 1 ? j : (int)__umulhi((uint32_t)j, wmagic)), w = j - pos * W, p = pid[pos];
       out[(size_t)(base[p] + (pos - (int)start[p])) * W + w] = stage[(size_t)srt[pos] * W + w];
     }
-    __syncthreads();
+    lds_sync();
     for (int i = tid; i < P; i += 1024) base[i] += cnt[i];
-    __syncthreads();
+    lds_sync();
   }
 }
 
