@@ -660,7 +660,9 @@ __device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* p
 // encoding) and the table is cleared for the next partition.
 __device__ __forceinline__ uint64_t spill_sext(int64_t v) { return v < 0 ? ~0ull : 0ull; }
 constexpr int kSpillPreU = 4;  // spill_agg_kernel: records per thread and step
-constexpr int kSpillPreW = 8;  // record words held in registers (launch_spill_* require spill_words <= 8)
+constexpr int kSpillPreW = 8;  // record words at most (launch_spill_* require spill_words <= 8)
+// WW = the record's words (spill_words), a template parameter so a step's records take WW registers each, not 8
+template <int WW>
 __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long long* recs, const int64_t* part_begin,
                                                          int P, int nw, int W, int S, DevQuery q, DevHash H,
                                                          uint64_t* acc, uint32_t narrow) {
@@ -696,10 +698,10 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
     for (int i = tid; i < nacc * S; i += blockDim.x) LA[i] = acc_identity(q.acc_op[i / S]);
     __syncthreads();
     // one record (its words in rw, statically indexed) into the partition's LDS table, or the HBM table
-    auto agg_one = [&](const uint64_t (&rw)[kSpillPreW]) {
+    auto agg_one = [&](const uint64_t (&rw)[WW]) {
       uint64_t kw[kMaxKeyWords];
 #pragma unroll
-      for (int w = 0; w < kSpillPreW; ++w)
+      for (int w = 0; w < WW; ++w)
         if (w < nw) kw[w] = rw[w];
       const uint64_t x = key_hash_rt(kw, nw);
       uint32_t s = (uint32_t)(((x & 0xFFFFFFFFull) * (uint64_t)(uint32_t)S) >> 32);
@@ -727,7 +729,7 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
       auto word = [&](int j) {  // record word j through selects (no dynamic register indexing)
         uint64_t v = 0ull;
 #pragma unroll
-        for (int w = 0; w < kSpillPreW; ++w) v = w == j ? rw[w] : v;
+        for (int w = 0; w < WW; ++w) v = w == j ? rw[w] : v;
         return v;
       };
       if (ls >= 0) {  // the LDS slot (the accumulator words addressed from the shared array: LDS atomics)
@@ -760,13 +762,13 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
     // kSpillPreU records per thread and step, every word loaded before any is aggregated (the loads of a step
     // overlap instead of each record's waiting behind the previous one's LDS atomics)
     for (int64_t i0 = r0; i0 < pe; i0 += (int64_t)kSpillPreU * blockDim.x) {
-      uint64_t rw[kSpillPreU][kSpillPreW];
+      uint64_t rw[kSpillPreU][WW];
 #pragma unroll
       for (int u = 0; u < kSpillPreU; ++u) {
         const int64_t i = i0 + (int64_t)u * blockDim.x + tid;
         const unsigned long long* r = recs + (i < pe ? i : r0) * W;
 #pragma unroll
-        for (int w = 0; w < kSpillPreW; ++w) rw[u][w] = w < W ? r[w] : 0ull;
+        for (int w = 0; w < WW; ++w) rw[u][w] = r[w];
       }
 #pragma unroll
       for (int u = 0; u < kSpillPreU; ++u)
@@ -1961,6 +1963,33 @@ hipError_t launch_segsel(const unsigned long long* keys, int64_t cap, int nw, co
   return hipGetLastError();
 }
 
+// spill_agg_kernel<W> for the record's width
+template <int WW>
+static hipError_t launch_spill_agg_w(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
+                                     int P, const DevQuery& q, uint64_t* acc, int agg_grid, int S, uint32_t narrow,
+                                     hipStream_t st) {
+  const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
+  (void)hipFuncSetAttribute((const void*)spill_agg_kernel<WW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(spill_agg_kernel<WW>, dim3((unsigned)agg_grid), dim3(1024), lds, st, sorted, part_begin, P, nw, WW,
+                     S, q, H, acc, narrow);
+  return hipGetLastError();
+}
+static hipError_t launch_spill_agg_kernel(const DevHash& H, int nw, const unsigned long long* sorted,
+                                          const int64_t* part_begin, int P, const DevQuery& q, uint64_t* acc,
+                                          int agg_grid, int S, uint32_t narrow, hipStream_t st) {
+  switch (H.spill_words) {
+    case 1: return launch_spill_agg_w<1>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 2: return launch_spill_agg_w<2>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 3: return launch_spill_agg_w<3>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 4: return launch_spill_agg_w<4>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 5: return launch_spill_agg_w<5>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 6: return launch_spill_agg_w<6>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 7: return launch_spill_agg_w<7>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    case 8: return launch_spill_agg_w<8>(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uint32_t* hist_unused, int64_t* offs,
                                int64_t* part_begin, unsigned long long* sorted, const DevQuery& q, uint64_t* acc,
                                int agg_grid, int S, int sorted_scatter, uint32_t narrow, hipStream_t st) {
@@ -1986,11 +2015,8 @@ hipError_t launch_spill_passes(const DevHash& H, int nw, int64_t grid, const uin
     hipLaunchKernelGGL(spill_scatter_kernel, dim3((unsigned)(grid * kSpillGroups)), dim3(1024), (size_t)P * 4, st, H, nw, grid,
                        (const int64_t*)offs, (const int64_t*)part_begin, sorted);
   }
-  const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
-  (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, (const unsigned long long*)sorted,
-                     (const int64_t*)part_begin, P, nw, H.spill_words, S, q, H, acc, narrow);
-  return hipGetLastError();
+  return launch_spill_agg_kernel(H, nw, (const unsigned long long*)sorted, (const int64_t*)part_begin, P, q, acc, agg_grid,
+                                 S, narrow, st);
 }
 
 // Direct placement's tables (DevHash::direct) from a region-mode execution's spill passes: record place
@@ -2018,11 +2044,7 @@ hipError_t launch_spill_direct_prep(const int64_t* offs, const int64_t* part_beg
 hipError_t launch_spill_agg(const DevHash& H, int nw, const unsigned long long* sorted, const int64_t* part_begin,
                             const DevQuery& q, uint64_t* acc, int agg_grid, int S, uint32_t narrow, hipStream_t st) {
   const int P = 1 << (64 - H.spill_shift);
-  const size_t lds = (size_t)S * (size_t)(nw + q.nacc) * 8;
-  (void)hipFuncSetAttribute((const void*)spill_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(spill_agg_kernel, dim3((unsigned)agg_grid), dim3(1024), lds, st, sorted, part_begin, P, nw,
-                     H.spill_words, S, q, H, acc, narrow);
-  return hipGetLastError();
+  return launch_spill_agg_kernel(H, nw, sorted, part_begin, P, q, acc, agg_grid, S, narrow, st);
 }
 
 hipError_t launch_seg_cut(const unsigned long long* bits, int64_t words, int32_t nsegs, int64_t limit,
