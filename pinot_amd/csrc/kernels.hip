@@ -659,7 +659,9 @@ __device__ __forceinline__ void spill_apply(int32_t op, uint64_t* p, uint64_t* p
 // slot is merged into the HBM table (AggregationFunction.merge: counts and sums add, MIN / MAX by the ordered
 // encoding) and the table is cleared for the next partition.
 __device__ __forceinline__ uint64_t spill_sext(int64_t v) { return v < 0 ? ~0ull : 0ull; }
-constexpr int kSpillPreU = 4;  // spill_agg_kernel: records per thread and step
+// spill_agg_kernel: records per thread and step, as many as ~24 record words of registers allow (4 for every width
+// before the kernel was templated on it)
+constexpr int spill_pre_u(int ww) { return 24 / ww < 2 ? 2 : 24 / ww > 8 ? 8 : 24 / ww; }
 constexpr int kSpillPreW = 8;  // record words at most (launch_spill_* require spill_words <= 8)
 // WW = the record's words (spill_words), a template parameter so a step's records take WW registers each, not 8
 template <int WW>
@@ -759,19 +761,19 @@ __global__ void __launch_bounds__(1024) spill_agg_kernel(const unsigned long lon
         spill_apply(op, base + (int64_t)a * stride, base + (int64_t)(a + 1 < nacc ? a + 1 : a) * stride, word(WJ[a]));
       }
     };
-    // kSpillPreU records per thread and step, every word loaded before any is aggregated (the loads of a step
+    // spill_pre_u(WW) records per thread and step, every word loaded before any is aggregated (the loads of a step
     // overlap instead of each record's waiting behind the previous one's LDS atomics)
-    for (int64_t i0 = r0; i0 < pe; i0 += (int64_t)kSpillPreU * blockDim.x) {
-      uint64_t rw[kSpillPreU][WW];
+    for (int64_t i0 = r0; i0 < pe; i0 += (int64_t)spill_pre_u(WW) * blockDim.x) {
+      uint64_t rw[spill_pre_u(WW)][WW];
 #pragma unroll
-      for (int u = 0; u < kSpillPreU; ++u) {
+      for (int u = 0; u < spill_pre_u(WW); ++u) {
         const int64_t i = i0 + (int64_t)u * blockDim.x + tid;
         const unsigned long long* r = recs + (i < pe ? i : r0) * W;
 #pragma unroll
         for (int w = 0; w < WW; ++w) rw[u][w] = r[w];
       }
 #pragma unroll
-      for (int u = 0; u < kSpillPreU; ++u)
+      for (int u = 0; u < spill_pre_u(WW); ++u)
         if (i0 + (int64_t)u * blockDim.x + tid < pe) agg_one(rw[u]);
     }
     __syncthreads();
