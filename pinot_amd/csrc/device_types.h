@@ -192,6 +192,12 @@ struct DevHash {
   unsigned long long* check;
   int32_t direct;
 };
+// A key's home slot in an HBM hash table of cap (a power of two) slots: the key hash's TOP bits, so the keys of one
+// spill partition (the same hash's top bits, DevHash::spill_shift) share one contiguous slice of the table and the
+// spill aggregation's merges of a partition land in a few MB of the table instead of all of it
+__host__ __device__ __forceinline__ uint64_t hash_home(uint64_t x, int64_t cap) {
+  return cap <= 1 ? 0ull : x >> (64 - __builtin_ctzll((unsigned long long)cap));
+}
 constexpr int kSpillMaxParts = 2048;  // spill partitions (the scan block's LDS histogram)
 // A scan block's spill region is split in kSpillGroups sub-regions by the partition's top 2 bits (sub-region
 // bx * kSpillGroups + g, spill_cap records each, spill_cnt per sub-region): a chunk of the region pass then meets a

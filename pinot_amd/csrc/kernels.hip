@@ -129,7 +129,7 @@ __device__ int64_t hash_find_rt(unsigned long long* keys, int64_t cap, int nw, c
   uint64_t x = 0x9E3779B97F4A7C15ull;
   for (int w = 0; w < nw; ++w) x = fmix64(x ^ kw[w]);
   const uint64_t mask = (uint64_t)cap - 1ull;
-  uint64_t i = x & mask;
+  uint64_t i = hash_home(x, cap);
   const int64_t lim = max_probe > 0 && max_probe < cap ? max_probe : cap;
   for (int64_t n = 0; n < lim; ++n) {
     bool ok = true;
