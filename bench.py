@@ -281,7 +281,7 @@ def main():
         # Issued 5 times (once when the group conversion alone is slow, e.g. ~1M groups): the median is reported,
         # the spread beside it (a single sample caught host outliers: one SSB query at 2.5 ms for a 1.0-ms median)
         samples = []
-        for _ in range(5 if cold_ms < 200 else 1):
+        for _ in range(5 if cold_ms < 200 and world == 1 else 1):  # (the same count on every rank)
             t_c = time.perf_counter()
             res2 = ex.execute(query, segs, stream=stream, key_space=ks)
             torch.cuda.synchronize()
