@@ -190,3 +190,31 @@ def test_widekeys_direct_placement_forced(wide, wide_uniform, env, monkeypatch):
             assert "+direct" in res.kernel_info(), res.kernel_info()
             assert res.groups() == exp
 
+
+
+_WIDTH_QUERIES = {  # spilled record width (key word + value words; COUNT is the record itself)
+    "w1": "SELECT w1, w2, w3, w4, w5, COUNT(*) FROM wide WHERE metInt < 900 GROUP BY w1, w2, w3, w4, w5",
+    "w2": "SELECT w1, w2, w3, w4, w5, COUNT(*), SUM(metInt) FROM wide GROUP BY w1, w2, w3, w4, w5",
+    "w5": ("SELECT w1, w2, w3, w4, w5, COUNT(*), SUM(metInt), MAX(metDouble), MIN(metDouble), MAX(metInt) "
+           "FROM wide WHERE metInt < 700 GROUP BY w1, w2, w3, w4, w5"),
+}
+
+
+@pytest.mark.parametrize("width", sorted(_WIDTH_QUERIES))
+def test_spill_record_widths_vs_oracle(wide, wide_uniform, width, monkeypatch):
+    """The spill passes at other record widths than the bench's 3 words: the region pass's register prefetch of
+    its next chunk and the aggregation templated on the width (kernels.hip spill_agg_kernel<W>), over skewed keys
+    (LDS level + spill) and uniform keys (the LDS level dropped after the first execution: every doc spilled).
+    COUNT, integer SUM and MIN / MAX are order-independent: exact."""
+    q = "SET numGroupsLimit = 2000000000; " + _WIDTH_QUERIES[width]
+    monkeypatch.setenv("PINOT_AMD_HASH_CAP_CACHE", "0")
+    monkeypatch.setenv("PINOT_AMD_HASH_DIRECT", "auto")
+    for E, bufs, segs, _ in (wide, wide_uniform):
+        _, exp = oracle.execute(q, bufs)
+        res = E.ServerQueryExecutor().execute(q, segs)
+        assert "hash" in res.kernel_info(), res.kernel_info()
+        assert res.groups() == exp
+        for _ in range(2):
+            res.execute_again()
+            assert res.groups() == exp
+            assert sum(v[0] for v in res.groups().values()) == res.num_docs_matched()
